@@ -1,0 +1,270 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s + wall-clock per frame at 1920x1080 on the ~100k-triangle synthetic OBJ
+(BASELINE.json metric; SURVEY.md §8d configuration C4: 8x8 grid of 40x21 UV spheres + back
+plane = 102,402 triangles, pf 1, max_lvl 3, lights (0,0,4) and (1.5,1.5,4)).
+
+A step renders one 1920x1080 frame's worth of 16x16 tiles per GPU: the step's batch is N frames
+of the same view whose tiles are interleaved over the N ranks (tile g -> rank g mod N), each rank
+renders its tiles with librtamd.so into HBM, and rank 0 collects them with one RCCL gather and
+un-permutes them on the device (weak scaling: fixed work per GPU). `--mode strong` instead splits
+ONE frame over the N ranks. A ray is one intersectMesh-equivalent query (primary + secondary +
+shadow), counted on the device.
+
+    python bench.py [--gpus N --steps K --warmup W]          # N>1: under torch.distributed.run
+
+Prints one JSON line on rank 0. See DESIGN.md §Measurement for the roofline and CPU-baseline
+definitions.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = "Mrays/s + wall-clock per frame at 1920×1080, 100k-tri OBJ"
+FLOP_PER_TEST = 37            # fp32 ops of rayIntersectTriangle's dominant path
+FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector (= FP32 matrix) peak
+HBM_PEAK_GBS = 8000.0
+WIDTH, HEIGHT, PF, MAX_LVL = 1920, 1080, 1, 3
+LIGHTS = ((0.0, 0.0, 4.0), (1.5, 1.5, 4.0))
+TILE = 16
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--mode", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--cpu-sample-every", type=int, default=96, help="CPU baseline: every k-th tile")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=1, help="steps re-run with HIP events for the roofline")
+    ap.add_argument("--ppm", default="", help="write the first frame to this PPM (rank 0)")
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world} differs from --gpus {args.gpus}; using WORLD_SIZE")
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import raytracert_amd as R
+    from raytracert_amd import dist as rdist, scenes
+    from raytracert_amd._capi import KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    tmp = tempfile.mkdtemp(prefix=f"rtbench_r{rank}_")
+    t_gen = time.time()
+    obj = scenes.write_sphere_grid(scenes.C4, tmp, "c4_sphere_grid")
+    t_gen = time.time() - t_gen
+    t_load = time.time()
+    scene = R.Scene.load(obj, device=local_rank)
+    t_load = time.time() - t_load
+    nv, nt, nm = scene.counts()
+    params = R.RenderParams(width=WIDTH, height=HEIGHT, pf=PF, max_lvl=MAX_LVL, lights=LIGHTS)
+    cparams = params.to_c()
+
+    layout = rdist.TileLayout(WIDTH, HEIGHT, TILE, TILE)
+    plan = rdist.ShardPlan(layout, world, frames=world if args.mode == "weak" else 1)
+    buf = torch.zeros(plan.shard_bytes, dtype=torch.uint8, device=dev)
+    index = torch.as_tensor(plan.gather_index(), device=dev)
+    calls = plan.calls(rank)
+    stream = torch.cuda.current_stream(dev)
+
+    def render_shard(want_counts=False):
+        off = 0
+        counts = np.zeros(3, np.uint64)
+        for (_, first, stride) in calls:
+            n_cap = (buf.numel() - off)
+            n, c = scene.render_tiles_device(cparams, TILE, TILE, first, stride, buf.data_ptr() + off, n_cap,
+                                             stream.cuda_stream, want_counts=want_counts)
+            off += n * layout.tile_bytes
+            if c is not None:
+                counts += c
+        return counts
+
+    def step():
+        render_shard()
+        gathered = rdist.gather_shards(buf, rank, world)
+        if rank == 0:
+            return rdist.assemble_plan_torch(gathered, plan, index)
+        return None
+
+    # rays per step (deterministic): counted once, summed over ranks
+    counts = render_shard(want_counts=True)
+    ct = torch.tensor([int(c) for c in counts], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(ct)
+    rays_per_step = float(ct.sum().item())
+    rays_by_kind = [int(x) for x in ct.tolist()]
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    # ---- timed region ----
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    frames = None
+    for _ in range(args.steps):
+        frames = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+
+    # ---- kernel timing for the roofline (HIP events on the scene's launch stream) ----
+    scene.reset_stats()
+    scene.set_profiling(True)
+    for _ in range(max(args.profile_steps, 1)):
+        render_shard()
+    torch.cuda.synchronize(dev)
+    scene.set_profiling(False)
+    ch_launches, ch_ms, ch_tests = scene.kernel_stats(KERNEL_CLOSEST_HIT)
+    sh_launches, sh_ms, sh_tests = scene.kernel_stats(KERNEL_SHADOW)
+    _, shade_ms, _ = scene.kernel_stats(KERNEL_SHADE)
+    _, frame_ms, _ = scene.kernel_stats(KERNEL_FRAME)
+
+    result = None
+    if rank == 0:
+        total_rays = rays_per_step * args.steps
+        value = total_rays / elapsed / 1e6
+        achieved = ch_tests * FLOP_PER_TEST / (ch_ms / 1e3) / 1e12 if ch_ms > 0 else 0.0
+        # algorithmic HBM bytes of the closest-hit kernel: each wave streams every 64-B triangle
+        # record once (scalar loads) and reads/writes its 64 queries (32 B in, 20 B out each)
+        ch_bytes = ch_tests / 64.0 * 64.0 + (ch_tests / max(nt, 1)) * 52.0
+        result = {
+            "metric": METRIC,
+            "value": round(value, 4),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak" if args.mode == "weak" else "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": "C4: synthetic 8x8 UV-sphere grid OBJ (102,402 tris) 1920x1080, pf 1, depth 3, 2 lights",
+                "frames_per_step": plan.frames,
+                "width": WIDTH, "height": HEIGHT, "pf": PF, "max_lvl": MAX_LVL, "lights": [list(l) for l in LIGHTS],
+                "triangles": nt, "vertices": nv, "tile": TILE,
+                "parallelism": f"tile-shard{world}",
+                "rays_per_step": int(rays_per_step),
+                "rays_by_kind_per_step": {"primary": rays_by_kind[0], "secondary": rays_by_kind[1], "shadow": rays_by_kind[2]},
+                "frame_ms_per_gpu": round(elapsed / args.steps * 1e3, 3),
+                "scene_load_s": round(t_load, 3), "scene_gen_s": round(t_gen, 3),
+            },
+            "roofline": {
+                "kernel": "k_closest_hit (primary + secondary queries, brute force)",
+                "bound": "valu",
+                "achieved": round(achieved, 3),
+                "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                "traffic": None,
+                "launches": ch_launches,
+                "avg_launch_ms": round(ch_ms / max(ch_launches, 1), 3),
+                "tests_per_launch": round(ch_tests / max(ch_launches, 1)),
+                "flop_per_test": FLOP_PER_TEST,
+                "hbm_algorithmic_GBps": round(ch_bytes / (ch_ms / 1e3) / 1e9, 2) if ch_ms > 0 else None,
+                "hbm_peak_GBps": HBM_PEAK_GBS,
+            },
+            "kernel_ms_per_step": {
+                "closest_hit": round(ch_ms / max(args.profile_steps, 1), 3),
+                "shadow": round(sh_ms / max(args.profile_steps, 1), 3),
+                "shade": round(shade_ms / max(args.profile_steps, 1), 3),
+                "frame": round(frame_ms / max(args.profile_steps, 1), 3),
+            },
+            "cpu_baseline": None,
+        }
+        if args.ppm and frames is not None:
+            R.write_ppm(args.ppm, frames[0].cpu().numpy())
+
+    # ---- CPU baseline + in-run parity on a bounded tile sample (rank 0, N=1 only) ----
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(obj, params, frames[0].cpu().numpy(), layout, args)
+
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+def cpu_baseline(obj, params, gpu_frame, layout, args):
+    """Time the CPU restatement (oracle/, 'port') on every k-th 16x16 tile of the same frame with
+    --cpu-threads threads, and check the GPU's bytes on those tiles against it."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import oracle as O
+    sc = O.OracleScene(obj)
+    op = O.make_params(params.width, params.height, params.pf, params.max_lvl, lights=params.lights)
+    tiles = list(range(0, layout.n_tiles, args.cpu_sample_every))
+    threads = args.cpu_threads
+    rays = 0
+    max_d = 0
+    exact = 0
+    total = 0
+    t0 = time.perf_counter()
+    outs = []
+    for t in tiles:
+        ty, tx = divmod(t, layout.tiles_x)
+        x0, y0 = tx * layout.tile_w, ty * layout.tile_h
+        w = min(layout.tile_w, params.width - x0)
+        h = min(layout.tile_h, params.height - y0)
+        _, u8, c = sc.render(op, x0, y0, w, h, nthreads=threads)
+        rays += int(c.sum())
+        outs.append((x0, y0, w, h, u8))
+    dt = time.perf_counter() - t0
+    for x0, y0, w, h, u8 in outs:
+        g = gpu_frame[y0:y0 + h, x0:x0 + w]
+        d = np.abs(g.astype(np.int16) - u8.astype(np.int16))
+        max_d = max(max_d, int(d.max()))
+        exact += int((d == 0).sum())
+        total += d.size
+    import platform
+    return {
+        "value": round(rays / dt / 1e6, 6),
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{len(tiles)} of {layout.n_tiles} 16x16 tiles (every {args.cpu_sample_every}th) of the same "
+                  f"C4 frame, {rays} rays in {dt:.1f} s, oracle/rt_oracle.c (-O2) on {threads} threads, "
+                  f"host {platform.processor() or platform.machine()}",
+        "parity_vs_gpu": {"bytes": total, "exact_frac": round(exact / max(total, 1), 6), "max_lsb": max_d},
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,157 @@
+/*
+ * raytracert.h — C-ABI of librtamd.so, the MI355X (gfx950) drop-in for the render path of
+ * wmorssink/raytracert (CG_Project). Plain pointers and sizes only; no HIP or torch types.
+ *
+ * Reference interface each entry replaces (paths relative to the reference's CG_Project/):
+ *   rt_scene_load_obj     init(char*)                       raytracing.h:19, raytracing.cpp:42-73
+ *                         Mesh::loadMesh / Mesh::loadMtl    mesh.h:176-177, mesh.cpp:95-460
+ *                         calculateNormals()                raytracing.h:41, raytracing.cpp:78-86
+ *   rt_scene_create       Mesh(vertices, triangles) ctor    mesh.h:175 (+ materials, mesh.h:197-200)
+ *   rt_scene_destroy      (globals live for the process: main.cpp:17-18,130)
+ *   rt_scene_export       read access to MyMesh / normals   raytracing.h:8, raytracing.cpp:33
+ *   rt_get_material       Material getMaterial(int)         raytracing.h:27, raytracing.cpp:373-376
+ *   rt_intersect_mesh     intersectMesh (batched)           raytracing.cpp:161-192
+ *   rt_trace_rays         Vec3Df performRayTracing(o, d)    raytracing.h:33, raytracing.cpp:410-416
+ *                         (batched; also trace(o,d,lvl) at lvl 0, raytracing.h:30)
+ *   rt_render_tile        the 'r'-key frame loop            main.cpp:340-411 (loop :355-395,
+ *                         + RGBValue clamp :24-42 + Image::writeImage quantisation :102-128)
+ *   rt_render_tiles_device  same loop, interleaved tile shard into a device buffer (multi-GPU)
+ *   rt_default_corners    produceRay for the 4 corners      main.cpp:300-325,355-358 (+ reshape :288-296)
+ *   rt_write_ppm          Image::writeImage                 main.cpp:102-128
+ *
+ * Errors: the reference has none (loadMesh returns true always, mesh.cpp:330; a missing OBJ
+ * crashes at fclose(NULL), mesh.cpp:329). Here every entry returns RT_OK (0) or a negative
+ * RT_E_* code, and rt_last_error_string() describes the last failure on the calling thread.
+ */
+#ifndef RAYTRACERT_H
+#define RAYTRACERT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_OK        0
+#define RT_E_IO     -1   /* OBJ cannot be opened / PPM cannot be written */
+#define RT_E_PARSE  -2   /* malformed input the reference would read out of bounds */
+#define RT_E_HIP    -3   /* a HIP runtime call or kernel launch failed */
+#define RT_E_ARG    -4   /* invalid argument (NULL, negative size, bad tile, too many lights) */
+#define RT_E_NOMEM  -5
+#define RT_E_NODEV  -6   /* no usable gfx950 device */
+
+#define RT_MAX_LIGHTS 16
+
+/* Feature switches (raytracing.cpp:15-20; keyboard keys 1-6, raytracing.cpp:456-473). */
+#define RT_AMBIENT    (1u << 0)
+#define RT_DIFFUSE    (1u << 1)
+#define RT_SPECULAR   (1u << 2)
+#define RT_REFLECTION (1u << 3)
+#define RT_SHADOWS    (1u << 4)
+#define RT_REFRACTION (1u << 5)
+#define RT_ALL_FEATURES 0x3Fu
+
+/* Material "is set" flags (mesh.h:116-122). */
+#define RT_HAS_KD    (1u << 0)
+#define RT_HAS_KA    (1u << 1)
+#define RT_HAS_KS    (1u << 2)
+#define RT_HAS_NS    (1u << 3)
+#define RT_HAS_NI    (1u << 4)
+#define RT_HAS_TR    (1u << 5)
+#define RT_HAS_ILLUM (1u << 6)
+
+/* Layout-compatible with Vec3Df (Vec3D.h:272,291: float p[3], 12 bytes). */
+typedef struct { float x, y, z; } rt_vec3;
+
+/* Material (mesh.h:10-125) as plain data. Values of never-set fields are defined as 0. */
+typedef struct {
+    float Kd[3], Ka[3], Ks[3];
+    float Ns, Ni, Tr;
+    int32_t illum;
+    uint32_t flags;      /* RT_HAS_* */
+} rt_material;
+
+/* Everything the reference reads from globals during a render. */
+typedef struct {
+    int32_t width, height;        /* WindowSize_X / WindowSize_Y (main.cpp:137-138) */
+    int32_t pfx, pfy;             /* pixelfactorX / pixelfactorY (raytracing.cpp:23-25), >= 1 */
+    int32_t max_lvl;              /* max recursion level (raytracing.cpp:29), >= 0 */
+    uint32_t flags;               /* RT_AMBIENT ... RT_REFRACTION */
+    int32_t n_lights;             /* MyLightPositions.size(), 0..RT_MAX_LIGHTS */
+    int32_t reserved;             /* must be 0 */
+    float lights[RT_MAX_LIGHTS][3];
+    float camera_pos[3];          /* MyCameraPosition (raytracing.h:10) */
+    float corners[8][3];          /* origin00,dest00, origin01,dest01, origin10,dest10, origin11,dest11 */
+} rt_params;
+
+typedef struct rt_scene rt_scene;
+
+/* Pass as `device` to load/create a scene on the host only (loader and inspection; no HIP calls).
+ * Render/intersect entries on such a scene return RT_E_NODEV. */
+#define RT_HOST_ONLY (-1)
+
+const char *rt_last_error_string(void);
+/* Number of visible HIP devices. */
+int rt_device_count(int32_t *count);
+
+/* ---- scene ---------------------------------------------------------------------------- */
+int  rt_scene_load_obj(const char *path, int32_t device, rt_scene **out);
+int  rt_scene_create(const float *xyz, int32_t n_vertices, const uint32_t *tri_v, const uint32_t *tri_mat,
+                     int32_t n_triangles, const rt_material *materials, int32_t n_materials,
+                     int32_t device, rt_scene **out);
+void rt_scene_destroy(rt_scene *scene);
+int  rt_scene_info(const rt_scene *scene, int32_t *n_vertices, int32_t *n_triangles, int32_t *n_materials);
+/* Host copies of the loaded scene; any pointer may be NULL. Sizes: 3*nv, 3*nt, nt, nm, 3*nt. */
+int  rt_scene_export(const rt_scene *scene, float *vertices, uint32_t *tri_v, uint32_t *tri_mat,
+                     rt_material *materials, float *face_normals);
+int  rt_get_material(const rt_scene *scene, int32_t triangle_index, rt_material *out);
+
+/* ---- hot path ------------------------------------------------------------------------- */
+/* Batched intersectMesh: n rays (origin[i], dest[i], host arrays of 3*n floats).
+ * index_out[i] = closest triangle or -1; point_out[3*i..] = hit point or (0,0,0). */
+int rt_intersect_mesh(rt_scene *scene, const float *origins, const float *dests, int32_t n,
+                      int32_t *index_out, float *point_out);
+/* Batched performRayTracing: rgb_out[3*i..] = unclamped colour of ray i.
+ * counts (may be NULL) receives {primary, secondary, shadow} intersectMesh-equivalent queries. */
+int rt_trace_rays(rt_scene *scene, const rt_params *params, const float *origins, const float *dests,
+                  int32_t n, float *rgb_out, uint64_t counts[3]);
+/* The frame loop for pixels [x0,x0+w) x [y0,y0+h) of the params->width x params->height frame.
+ * rgb_u8 (w*h*3 bytes, row-major, top row first, as written to result.ppm) and rgb_f32
+ * (w*h*3 clamped floats) are host buffers; either may be NULL. */
+int rt_render_tile(rt_scene *scene, const rt_params *params, int32_t x0, int32_t y0, int32_t w, int32_t h,
+                   uint8_t *rgb_u8, float *rgb_f32, uint64_t counts[3]);
+/* Interleaved tile shard for multi-GPU rendering, fully device-resident. The frame is cut into
+ * tile_w x tile_h tiles numbered row-major (tiles_x = ceil(width/tile_w)); this call renders tiles
+ * first, first+stride, first+2*stride, ... and writes each as tile_w*tile_h*3 bytes (pixels outside
+ * the frame are 0) into the DEVICE buffer d_out_u8 in that order. stream is a hipStream_t (NULL =
+ * the scene's own stream); the call returns after enqueueing (no host synchronisation) unless
+ * counts != NULL. Returns the number of tiles written via n_tiles_out. */
+int rt_render_tiles_device(rt_scene *scene, const rt_params *params, int32_t tile_w, int32_t tile_h,
+                           int32_t first, int32_t stride, void *d_out_u8, size_t out_capacity,
+                           void *stream, int32_t *n_tiles_out, uint64_t counts[3]);
+
+/* ---- helpers -------------------------------------------------------------------------- */
+/* Corner rays of the reference's default view (camera at (0,0,4), fovy 50, near 1, far 10). */
+int rt_default_corners(int32_t width, int32_t height, float corners[8][3]);
+/* Image::writeImage: "P6\n%i %i\n255\n" + w*h*3 bytes. */
+int rt_write_ppm(const char *path, int32_t width, int32_t height, const uint8_t *rgb_u8);
+
+/* ---- measurement ---------------------------------------------------------------------- */
+/* Kernel kinds for rt_kernel_stats. */
+#define RT_KERNEL_CLOSEST_HIT 0   /* closest-hit over all triangles (primary + secondary queries) */
+#define RT_KERNEL_SHADOW      1   /* shadow queries (closest-hit or any-hit) */
+#define RT_KERNEL_SHADE       2   /* shading / secondary-ray generation */
+#define RT_KERNEL_FRAME       3   /* sample generation + fold + AA + quantise */
+#define RT_KERNEL_KINDS       4
+/* When enabled, every launch of the scene is bracketed with hipEvents on its own stream and the
+ * durations accumulated (one host sync per render call). */
+int rt_set_profiling(rt_scene *scene, int32_t enabled);
+/* launches, summed milliseconds, and summed ray-triangle tests (closest-hit/shadow kinds). */
+int rt_kernel_stats(rt_scene *scene, int32_t kind, uint64_t *launches, double *total_ms, double *tests);
+int rt_reset_stats(rt_scene *scene);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,111 @@
+"""ctypes binding of librtamd.so (include/raytracert.h).
+
+The library is built in-tree (raytracert_amd/librtamd.so, `make -C raytracert_amd`). There is
+no fallback: if the shared object is missing or fails to load, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librtamd.so")
+HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "raytracert.h")
+
+RT_OK = 0
+RT_E_IO = -1
+RT_E_PARSE = -2
+RT_E_HIP = -3
+RT_E_ARG = -4
+RT_E_NOMEM = -5
+RT_E_NODEV = -6
+RT_HOST_ONLY = -1
+RT_MAX_LIGHTS = 16
+
+AMBIENT, DIFFUSE, SPECULAR, REFLECTION, SHADOWS, REFRACTION = (1 << i for i in range(6))
+ALL_FEATURES = 0x3F
+
+HAS_KD, HAS_KA, HAS_KS, HAS_NS, HAS_NI, HAS_TR, HAS_ILLUM = (1 << i for i in range(7))
+
+KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME = range(4)
+
+
+class RtParams(C.Structure):
+    _fields_ = [
+        ("width", C.c_int32), ("height", C.c_int32),
+        ("pfx", C.c_int32), ("pfy", C.c_int32),
+        ("max_lvl", C.c_int32), ("flags", C.c_uint32),
+        ("n_lights", C.c_int32), ("reserved", C.c_int32),
+        ("lights", (C.c_float * 3) * RT_MAX_LIGHTS),
+        ("camera_pos", C.c_float * 3),
+        ("corners", (C.c_float * 3) * 8),
+    ]
+
+
+class RtMaterial(C.Structure):
+    _fields_ = [
+        ("Kd", C.c_float * 3), ("Ka", C.c_float * 3), ("Ks", C.c_float * 3),
+        ("Ns", C.c_float), ("Ni", C.c_float), ("Tr", C.c_float),
+        ("illum", C.c_int32), ("flags", C.c_uint32),
+    ]
+
+
+class RtError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"rt error {code}: {message}")
+        self.code = code
+
+
+_VP = C.c_void_p
+_SIGNATURES = {
+    "rt_last_error_string": ([], C.c_char_p),
+    "rt_device_count": ([C.POINTER(C.c_int32)], C.c_int),
+    "rt_scene_load_obj": ([C.c_char_p, C.c_int32, C.POINTER(_VP)], C.c_int),
+    "rt_scene_create": ([_VP, C.c_int32, _VP, _VP, C.c_int32, _VP, C.c_int32, C.c_int32, C.POINTER(_VP)], C.c_int),
+    "rt_scene_destroy": ([_VP], None),
+    "rt_scene_info": ([_VP, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)], C.c_int),
+    "rt_scene_export": ([_VP, _VP, _VP, _VP, _VP, _VP], C.c_int),
+    "rt_get_material": ([_VP, C.c_int32, C.POINTER(RtMaterial)], C.c_int),
+    "rt_intersect_mesh": ([_VP, _VP, _VP, C.c_int32, _VP, _VP], C.c_int),
+    "rt_trace_rays": ([_VP, C.POINTER(RtParams), _VP, _VP, C.c_int32, _VP, _VP], C.c_int),
+    "rt_render_tile": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP, _VP, _VP], C.c_int),
+    "rt_render_tiles_device": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP, C.c_size_t,
+                                _VP, C.POINTER(C.c_int32), _VP], C.c_int),
+    "rt_default_corners": ([C.c_int32, C.c_int32, _VP], C.c_int),
+    "rt_write_ppm": ([C.c_char_p, C.c_int32, C.c_int32, _VP], C.c_int),
+    "rt_set_profiling": ([_VP, C.c_int32], C.c_int),
+    "rt_kernel_stats": ([_VP, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.POINTER(C.c_double)], C.c_int),
+    "rt_reset_stats": ([_VP], C.c_int),
+}
+
+_lib = None
+
+
+def header_symbols(path: str = HEADER_PATH) -> list[str]:
+    """Function names declared in include/raytracert.h."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z_0-9]+)\s*\(", text)))
+
+
+def lib() -> C.CDLL:
+    """Load librtamd.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with `make -C raytracert_amd` "
+                              "(or __graft_entry__.build()); there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        for name, (args, res) in _SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != RT_OK:
+        msg = lib().rt_last_error_string()
+        raise RtError(rc, msg.decode() if msg else "")

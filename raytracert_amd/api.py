@@ -1,0 +1,214 @@
+"""Python mirror of the reference's render-path interface, over the C-ABI.
+
+Reference names kept (CG_Project/raytracing.h): `init` -> Scene.load (raytracing.h:19),
+`intersectMesh` -> Scene.intersect_mesh (raytracing.cpp:161), `performRayTracing` ->
+Scene.perform_ray_tracing (raytracing.h:33), `getMaterial` -> Scene.get_material
+(raytracing.h:27), the 'r' key -> Scene.render (main.cpp:340-411), `produceRay` corners ->
+default_corners (main.cpp:300-325), `Image::writeImage` -> write_ppm (main.cpp:102-128).
+Every call goes to librtamd.so; errors raise RtError with the library's message.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Sequence
+
+import numpy as np
+
+from . import _capi
+from ._capi import ALL_FEATURES, RT_HOST_ONLY, RtMaterial, RtParams, check, lib
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def default_corners(width: int, height: int) -> np.ndarray:
+    """The 8 corner vectors produceRay yields for the default view (origin00, dest00, origin01,
+    dest01, origin10, dest10, origin11, dest11)."""
+    out = np.zeros((8, 3), np.float32)
+    check(lib().rt_default_corners(width, height, _ptr(out)))
+    return out
+
+
+def write_ppm(path: str, rgb_u8: np.ndarray) -> None:
+    rgb = np.ascontiguousarray(rgb_u8, np.uint8)
+    h, w = rgb.shape[:2]
+    check(lib().rt_write_ppm(path.encode(), w, h, _ptr(rgb)))
+
+
+@dataclass
+class RenderParams:
+    """Everything the reference reads from globals during a render (raytracing.cpp:15-29,
+    raytracing.h:9-16). Defaults are the reference's own: pixelfactor 3, max_lvl 10, every
+    feature on, one light at the camera position (0,0,4)."""
+    width: int = 500
+    height: int = 500
+    pf: int = 3
+    max_lvl: int = 10
+    lights: Sequence[Sequence[float]] = ((0.0, 0.0, 4.0),)
+    flags: int = ALL_FEATURES
+    camera_pos: Sequence[float] = (0.0, 0.0, 4.0)
+    corners: np.ndarray | None = field(default=None, repr=False)
+
+    def to_c(self) -> RtParams:
+        if len(self.lights) > _capi.RT_MAX_LIGHTS:
+            raise ValueError("at most 16 lights")
+        p = RtParams()
+        p.width, p.height, p.pfx, p.pfy = self.width, self.height, self.pf, self.pf
+        p.max_lvl, p.flags, p.n_lights = self.max_lvl, self.flags, len(self.lights)
+        for i, l in enumerate(self.lights):
+            for k in range(3):
+                p.lights[i][k] = float(l[k])
+        for k in range(3):
+            p.camera_pos[k] = float(self.camera_pos[k])
+        cs = default_corners(self.width, self.height) if self.corners is None else np.asarray(self.corners, np.float32)
+        for i in range(8):
+            for k in range(3):
+                p.corners[i][k] = float(cs[i, k])
+        return p
+
+
+class Scene:
+    """A loaded mesh bound to one GPU (or host-only with device=-1)."""
+
+    def __init__(self, handle: C.c_void_p, device: int):
+        self._h = handle
+        self.device = device
+
+    # -- construction ------------------------------------------------------------------------
+    @classmethod
+    def load(cls, path: str, device: int = 0) -> "Scene":
+        """init(fileName): Mesh::loadMesh + loadMtl + calculateNormals."""
+        h = C.c_void_p()
+        check(lib().rt_scene_load_obj(path.encode(), device, C.byref(h)))
+        return cls(h, device)
+
+    @classmethod
+    def create(cls, vertices, triangles, tri_mat, materials: Sequence[dict], device: int = 0) -> "Scene":
+        v = np.ascontiguousarray(vertices, np.float32).reshape(-1, 3)
+        t = np.ascontiguousarray(triangles, np.uint32).reshape(-1, 3)
+        m = np.ascontiguousarray(tri_mat, np.uint32).reshape(-1)
+        mats = (RtMaterial * len(materials))()
+        for i, d in enumerate(materials):
+            for k in range(3):
+                mats[i].Kd[k] = d.get("Kd", (0, 0, 0))[k]
+                mats[i].Ka[k] = d.get("Ka", (0, 0, 0))[k]
+                mats[i].Ks[k] = d.get("Ks", (0, 0, 0))[k]
+            mats[i].Ns, mats[i].Ni, mats[i].Tr = d.get("Ns", 0.0), d.get("Ni", 0.0), d.get("Tr", 0.0)
+            mats[i].illum, mats[i].flags = d.get("illum", 0), d.get("flags", 0)
+        h = C.c_void_p()
+        check(lib().rt_scene_create(_ptr(v), len(v), _ptr(t), _ptr(m), len(m), C.cast(mats, C.c_void_p),
+                                    len(materials), device, C.byref(h)))
+        return cls(h, device)
+
+    def close(self) -> None:
+        if self._h:
+            lib().rt_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    # -- inspection --------------------------------------------------------------------------
+    def counts(self) -> tuple[int, int, int]:
+        nv, nt, nm = C.c_int32(), C.c_int32(), C.c_int32()
+        check(lib().rt_scene_info(self._h, C.byref(nv), C.byref(nt), C.byref(nm)))
+        return nv.value, nt.value, nm.value
+
+    def export(self) -> dict:
+        nv, nt, nm = self.counts()
+        verts = np.zeros((nv, 3), np.float32)
+        tri = np.zeros((nt, 3), np.uint32)
+        tmat = np.zeros(nt, np.uint32)
+        normals = np.zeros((nt, 3), np.float32)
+        mats = (RtMaterial * max(nm, 1))()
+        check(lib().rt_scene_export(self._h, _ptr(verts), _ptr(tri), _ptr(tmat), C.cast(mats, C.c_void_p), _ptr(normals)))
+        mat_list = [dict(Kd=tuple(m.Kd), Ka=tuple(m.Ka), Ks=tuple(m.Ks), Ns=m.Ns, Ni=m.Ni, Tr=m.Tr,
+                         illum=m.illum, flags=m.flags) for m in list(mats)[:nm]]
+        return dict(vertices=verts, triangles=tri, tri_mat=tmat, materials=mat_list, normals=normals)
+
+    def get_material(self, triangle_index: int) -> dict:
+        m = RtMaterial()
+        check(lib().rt_get_material(self._h, triangle_index, C.byref(m)))
+        return dict(Kd=tuple(m.Kd), Ka=tuple(m.Ka), Ks=tuple(m.Ks), Ns=m.Ns, Ni=m.Ni, Tr=m.Tr,
+                    illum=m.illum, flags=m.flags)
+
+    # -- hot path ----------------------------------------------------------------------------
+    def intersect_mesh(self, origins, dests):
+        """Batched intersectMesh: returns (index[n] int32, point[n,3] float32)."""
+        o = np.ascontiguousarray(origins, np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(dests, np.float32).reshape(-1, 3)
+        n = len(o)
+        idx = np.zeros(n, np.int32)
+        pts = np.zeros((n, 3), np.float32)
+        check(lib().rt_intersect_mesh(self._h, _ptr(o), _ptr(d), n, _ptr(idx), _ptr(pts)))
+        return idx, pts
+
+    def perform_ray_tracing(self, params: RenderParams, origins, dests):
+        """Batched performRayTracing: returns (rgb[n,3] float32 unclamped, counts[3])."""
+        o = np.ascontiguousarray(origins, np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(dests, np.float32).reshape(-1, 3)
+        n = len(o)
+        rgb = np.zeros((n, 3), np.float32)
+        counts = np.zeros(3, np.uint64)
+        p = params.to_c()
+        check(lib().rt_trace_rays(self._h, C.byref(p), _ptr(o), _ptr(d), n, _ptr(rgb), _ptr(counts)))
+        return rgb, counts
+
+    def render(self, params: RenderParams, x0: int = 0, y0: int = 0, w: int | None = None, h: int | None = None,
+               want_f32: bool = False):
+        """The 'r' key for a pixel rectangle: returns (u8[h,w,3], f32[h,w,3] or None, counts[3])."""
+        w = params.width - x0 if w is None else w
+        h = params.height - y0 if h is None else h
+        u8 = np.zeros((h, w, 3), np.uint8)
+        f32 = np.zeros((h, w, 3), np.float32) if want_f32 else None
+        counts = np.zeros(3, np.uint64)
+        p = params.to_c()
+        check(lib().rt_render_tile(self._h, C.byref(p), x0, y0, w, h, _ptr(u8), _ptr(f32), _ptr(counts)))
+        return u8, f32, counts
+
+    def render_tiles_device(self, params: RenderParams | RtParams, tile_w: int, tile_h: int, first: int, stride: int,
+                            out_ptr: int, out_capacity: int, stream_ptr: int | None = None, want_counts: bool = False):
+        """Interleaved tile shard into a device buffer (e.g. a torch uint8 CUDA tensor's data_ptr())."""
+        p = params.to_c() if isinstance(params, RenderParams) else params
+        n_tiles = C.c_int32()
+        counts = np.zeros(3, np.uint64) if want_counts else None
+        check(lib().rt_render_tiles_device(self._h, C.byref(p), tile_w, tile_h, first, stride, C.c_void_p(out_ptr),
+                                           out_capacity, C.c_void_p(stream_ptr) if stream_ptr else None,
+                                           C.byref(n_tiles), _ptr(counts)))
+        return n_tiles.value, counts
+
+    # -- measurement -------------------------------------------------------------------------
+    def set_profiling(self, enabled: bool) -> None:
+        check(lib().rt_set_profiling(self._h, 1 if enabled else 0))
+
+    def kernel_stats(self, kind: int) -> tuple[int, float, float]:
+        launches, ms, tests = C.c_uint64(), C.c_double(), C.c_double()
+        check(lib().rt_kernel_stats(self._h, kind, C.byref(launches), C.byref(ms), C.byref(tests)))
+        return launches.value, ms.value, tests.value
+
+    def reset_stats(self) -> None:
+        check(lib().rt_reset_stats(self._h))
+
+
+def device_count() -> int:
+    n = C.c_int32()
+    check(lib().rt_device_count(C.byref(n)))
+    return n.value
+
+
+__all__ = ["Scene", "RenderParams", "default_corners", "write_ppm", "device_count", "RT_HOST_ONLY"]

@@ -1,0 +1,67 @@
+// rt_internal.h — host-side scene model and device-side record layouts shared by the loader,
+// the render driver (rt_capi.cpp) and the kernels (rt_kernels.hip).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "raytracert.h"
+
+namespace rt {
+
+// ---- host scene (Mesh, mesh.h:172-201, plus the face normals of raytracing.cpp:33) ---------
+struct HostMaterial {
+    float Kd[3] = {0, 0, 0}, Ka[3] = {0, 0, 0}, Ks[3] = {0, 0, 0};
+    float Ns = 0, Ni = 0, Tr = 0;
+    int32_t illum = 0;
+    uint32_t flags = 0;
+    std::string name;
+};
+
+struct HostScene {
+    std::vector<float> verts;        // 3 per vertex
+    std::vector<uint32_t> tris;      // 3 per triangle
+    std::vector<uint32_t> tri_mat;   // per triangle
+    std::vector<HostMaterial> mats;  // index 0 = default material (mesh.cpp:108-117)
+    std::vector<float> normals;      // 3 per triangle (calculateNormals, raytracing.cpp:78-86)
+};
+
+// OBJ/MTL loader with Mesh::loadMesh / loadMtl semantics (mesh.cpp:95-460).
+// Returns RT_OK or RT_E_IO; warnings go to stderr like the reference's printf.
+int load_obj(const char *path, HostScene &out, std::string &err);
+// calculateNormals (raytracing.cpp:78-86), binary32 without contraction.
+void compute_face_normals(HostScene &s);
+
+// ---- device layouts -----------------------------------------------------------------------
+// One triangle = 4 x float4 = 64 B, every ray-independent quantity of rayIntersectTriangle
+// (raytracing.cpp:106-108,134-136,140) hoisted; hoisting is bit-exact (same ops, same order).
+//   q0 = {T0.x, T0.y, T0.z, uu}   q1 = {u.x, u.y, u.z, uv}
+//   q2 = {v.x,  v.y,  v.z,  vv}   q3 = {n.x, n.y, n.z, D}
+struct alignas(16) TriRec {
+    float t0[3]; float uu;
+    float u[3];  float uv;
+    float v[3];  float vv;
+    float n[3];  float D;
+};
+static_assert(sizeof(TriRec) == 64, "TriRec must be 64 bytes");
+
+struct alignas(16) DevMaterial {
+    float Kd[3]; float Ns;
+    float Ka[3]; float Ni;
+    float Ks[3]; float Tr;
+    uint32_t flags;
+    float powf_nr2;      // glibc powf(1/Ni, 2)  (raytracing.cpp:302), precomputed on the host
+    float powf_ni2;      // glibc powf(Ni, 2)    (raytracing.cpp:316)
+    uint32_t transparent; // has_Tr && Tr < 1 (raytracing.cpp:254)
+};
+static_assert(sizeof(DevMaterial) == 64, "DevMaterial must be 64 bytes");
+
+void build_tri_records(const HostScene &s, std::vector<TriRec> &out);
+void build_dev_materials(const HostScene &s, std::vector<DevMaterial> &out);
+
+// glibc powf(x, 2) differs from the correctly rounded x*x exactly on the inputs listed in this
+// table (|x| < 2, sorted bit patterns of |x|); on each of them glibc returns the next float up.
+const uint32_t *powf2_tie_table(size_t *n);
+
+}  // namespace rt

@@ -1,0 +1,78 @@
+// rt_kernels.h — launch interface of the gfx950 kernels (rt_kernels.hip) used by the render
+// driver (rt_capi.cpp). Host-only declarations; no kernel code here.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "rt_internal.h"
+
+namespace rt {
+
+// Chain step states (how shade() combines a level with its child, raytracing.cpp:357-363)
+enum : uint32_t { kChildNone = 0, kChildTrace = 1, kChildZero = 2 };
+
+// Where samples come from and where finished pixels go.
+struct FrameGeom {
+    int32_t width, height, pfx, pfy;    // frame and sub-sample grid (main.cpp:347,360-362)
+    float divX, divY;                   // float(W*pf - 1), float(H*pf - 1)
+    int32_t tw, th, tiles_x;            // tile size and tiles per row of the tiled region
+    int32_t first, stride;              // tile id of batch tile i = first + (tile0 + i) * stride
+    int32_t tile0, ntiles;              // this batch
+    int32_t ox, oy, cw, ch;             // tiled region origin / clip size (absolute pixels)
+    int32_t out_mode;                   // 0: tile-major shard layout, 1: row-major in the clip rect
+    int32_t pad;
+    float corners[8][3];                // origin00,dest00,origin01,dest01,origin10,dest10,origin11,dest11
+};
+
+struct ShadeParams {
+    int32_t max_lvl;
+    uint32_t flags;
+    int32_t n_lights;
+    int32_t step;
+    float lights[RT_MAX_LIGHTS][3];
+    float cam[3];
+    float pad;
+};
+
+// Device views of one scene and one render workspace.
+struct DevScene {
+    const TriRec *tris;
+    const uint32_t *tri_mat;
+    const float4 *normals;          // xyz = face normal
+    const DevMaterial *mats;
+    const uint32_t *ties;           // powf(x,2) tie table
+    int32_t nt, nm, n_ties, any_transparent;
+};
+
+struct DevWork {
+    float4 *q_org[2], *q_dst[2];    // ping-pong main query queues; org.w = sample id, dst.w = lvl (int bits)
+    int32_t *hit_idx;
+    float4 *hit_I;
+    float4 *sq_org, *sq_dst;        // shadow queue; org.w = output slot (query * n_lights + light)
+    uint8_t *shadow;                // per (query, light): 1 = in shadow
+    float4 *chain_local;            // [step][sample]: xyz = local colour, w = child state (bits)
+    float4 *chain_coef;             // [step][sample]: xyz = coefficient on the child's colour
+    uint8_t *depth;                 // per sample: number of chain steps
+    int32_t *counters;              // [0..kMaxSteps] main queue counts, [kMaxSteps+1 ..] shadow counts
+    unsigned long long *rays;       // primary, secondary, shadow
+    int64_t cap;                    // samples per batch
+    int32_t steps;                  // chain steps allocated (max_lvl + 1)
+};
+
+constexpr int kMaxStepsCounters = 4096;   // counters[step] for main queues; [kMaxStepsCounters + step] shadow
+
+// Launchers (all asynchronous on `stream`).
+void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream);
+void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevWork &w, hipStream_t stream);
+void launch_closest_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream);
+void launch_shadow_gen(const DevScene &s, const DevWork &w, const ShadeParams &p, int64_t capacity, hipStream_t stream);
+void launch_shadow_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream);
+void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int64_t capacity, hipStream_t stream);
+void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream);
+void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t stream);
+void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *dst, int32_t n,
+                           int32_t *idx, float4 *I, hipStream_t stream);
+
+}  // namespace rt

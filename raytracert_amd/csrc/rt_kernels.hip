@@ -1,0 +1,570 @@
+// rt_kernels.hip — gfx950 kernels of the render path.
+//
+// Wavefront structure (one launch per stage, queues compacted with wave-aggregated atomics):
+//   gen_primary  -> main queue Q0 (one query per sub-sample; main.cpp:369-388)
+//   per chain step k = 0..max_lvl:
+//     closest_hit(Q_k)            intersectMesh, raytracing.cpp:161-192   <- the hot kernel
+//     shadow_gen + shadow_hit     isShadow, raytracing.cpp:241-261 (any-hit when no material is
+//                                 transparent, closest-hit + material test otherwise)
+//     shade(Q_k) -> Q_{k+1}       shade/diffuse/specular/reflection/refraction, :194-368
+//   frame        fold the chain back to front (trace() returns are consumed innermost first),
+//                AA average, RGBValue clamp, (unsigned char)(v*255) (main.cpp:24-42,389-393,117)
+//
+// Numerics: compiled with -ffp-contract=off; HIP's f32 '/' and sqrtf are correctly rounded on
+// gfx950 and f32 denormals are on, as on x86 SSE. Every expression keeps the reference's
+// operand order (Vec3D.h dot = (a0*b0 + a1*b1) + a2*b2). acosf and powf(x,2) of refraction()
+// are replaced by bit-exact equivalents of glibc (threshold / tie table, see below).
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdint>
+
+#include "rt_kernels.h"
+
+namespace rt {
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ int as_int(float f) { return __float_as_int(f); }
+__device__ __forceinline__ float as_float(int i) { return __int_as_float(i); }
+
+struct V3 { float x, y, z; };
+__device__ __forceinline__ V3 mk(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 neg(V3 a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ V3 scale(V3 a, float f) { return mk(a.x * f, a.y * f, a.z * f); }   // Vec3D.h:12-18
+__device__ __forceinline__ V3 mul(V3 a, V3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }  // Vec3D.h:20-22
+__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; } // Vec3D.h:192-194
+__device__ __forceinline__ void normalize(V3 &a) {                                                 // Vec3D.h:142-151
+    float len = sqrtf(dot(a, a));
+    if (len == 0.0f) return;
+    float rez = 1.0f / len;
+    a.x *= rez; a.y *= rez; a.z *= rez;
+}
+__device__ __forceinline__ float max_std(float a, float b) { return (a < b) ? b : a; }            // std::max
+__device__ __forceinline__ V3 ld3(const float4 &v) { return mk(v.x, v.y, v.z); }
+
+// acosf(check) in (0, 2] for check < 0 (raytracing.cpp:296-298): glibc's acosf crosses 2.0
+// exactly once on [-1, 0), at -0x1.aa226cp-2 (acosf of it is 2.0f); verified exhaustively by
+// tests/test_numerics.py::test_acos_threshold against this platform's libm.
+constexpr float kAcosLe2Threshold = -0x1.aa226cp-2f;
+
+// glibc powf(x, 2) (raytracing.cpp:302,316): x*x, moved one ulp where glibc differs (table from
+// gen_powf2_ties.c; bit 31 = down). |x| >= 2 is outside the table and returns x*x.
+__device__ float glibc_powf2(float x, const uint32_t *ties, int n) {
+    float r = x * x;
+    uint32_t ax = static_cast<uint32_t>(as_int(x)) & 0x7fffffffu;
+    if (ax >= 0x40000000u || n <= 0) return r;
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if ((ties[mid] & 0x7fffffffu) < ax) lo = mid + 1; else hi = mid;
+    }
+    if (lo < n && (ties[lo] & 0x7fffffffu) == ax) {
+        uint32_t rb = static_cast<uint32_t>(as_int(r));
+        rb = (ties[lo] >> 31) ? rb - 1u : rb + 1u;
+        r = as_float(static_cast<int>(rb));
+    }
+    return r;
+}
+
+// powf(SpecularTerm, Ns) (raytracing.cpp:226): evaluated in double and rounded once; agrees with
+// glibc powf except where glibc itself is not correctly rounded (colour-only, <= 1 LSB).
+__device__ __forceinline__ float spec_powf(float x, float y) {
+    return static_cast<float>(pow(static_cast<double>(x), static_cast<double>(y)));
+}
+
+// Wave-aggregated queue append: one atomic per wave, order within the wave preserved.
+__device__ __forceinline__ int wave_append(int32_t *counter, bool pred) {
+    const unsigned long long mask = __ballot(pred);
+    if (mask == 0) return -1;
+    const int lane = __lane_id();
+    const int leader = __ffsll(static_cast<long long>(mask)) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(counter, __popcll(mask));
+    base = __shfl(base, leader);
+    const unsigned long long below = mask & ((1ull << lane) - 1ull);
+    return pred ? base + __popcll(below) : -1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Closest hit: rayIntersectTriangle (raytracing.cpp:99-154) over every triangle in index order,
+// strict '<' on the distance (:183) so ties keep the lowest index. One lane = one query; the
+// triangle loop is wave-uniform, so each 64-byte record is fetched with scalar loads and the VALU
+// reads it from SGPRs (no VGPR/LDS copy).
+// ---------------------------------------------------------------------------------------------
+template <bool kAnyHit>
+__device__ __forceinline__ void closest_hit_loop(const TriRec *__restrict__ tris, int nt, V3 o, V3 dir, bool active,
+                                                 int &bidx, V3 &bI) {
+    float best = FLT_MAX;
+    bool done = !active;
+    for (int t = 0; t < nt; ++t) {
+        if (kAnyHit) {
+            if ((t & 15) == 0 && __all(done)) break;
+            if (done) continue;
+        }
+        const TriRec T = tris[t];
+        const V3 w0 = mk(o.x - T.t0[0], o.y - T.t0[1], o.z - T.t0[2]);
+        const float b = T.n[0] * dir.x + T.n[1] * dir.y + T.n[2] * dir.z;          // :113
+        const float a = -(T.n[0] * w0.x + T.n[1] * w0.y + T.n[2] * w0.z);          // :114
+        if (fabsf(b) < 0.00001f) continue;                                          // :115
+        const float r = a / b;                                                      // :124
+        if (r < 0) continue;                                                        // :125
+        const V3 I = mk(o.x + dir.x * r, o.y + dir.y * r, o.z + dir.z * r);         // :130
+        const V3 w = mk(I.x - T.t0[0], I.y - T.t0[1], I.z - T.t0[2]);               // :137
+        const float wu = w.x * T.u[0] + w.y * T.u[1] + w.z * T.u[2];                 // :138
+        const float wv = w.x * T.v[0] + w.y * T.v[1] + w.z * T.v[2];                 // :139
+        const float s = (T.uv * wv - T.vv * wu) / T.D;                              // :144
+        if (s < 0 || s > 1) continue;                                               // :145
+        const float tt = (T.uv * wu - T.uu * wv) / T.D;                             // :148
+        if (tt < 0 || (s + tt) > 1) continue;                                       // :149
+        const V3 e = sub(o, I);                                                     // distance, Vec3D.h:199-202
+        const float dist = sqrtf(dot(e, e));
+        if (dist < best) {                                                          // :183
+            best = dist; bidx = t; bI = I;
+            if (kAnyHit) done = true;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_closest_hit(const TriRec *__restrict__ tris, int nt,
+                                                        const float4 *__restrict__ q_org,
+                                                        const float4 *__restrict__ q_dst,
+                                                        const int32_t *__restrict__ q_count,
+                                                        int32_t *__restrict__ hit_idx, float4 *__restrict__ hit_I) {
+    const int n = *q_count;
+    const int base = blockIdx.x * kBlock;
+    if (base >= n) return;
+    const int j = base + threadIdx.x;
+    const bool active = j < n;
+    V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
+    if (active) {
+        const float4 qo = q_org[j], qd = q_dst[j];
+        o = mk(qo.x, qo.y, qo.z);
+        dir = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);                          // :111
+    }
+    int bidx = -1;
+    V3 bI = mk(0, 0, 0);
+    closest_hit_loop<false>(tris, nt, o, dir, active, bidx, bI);
+    if (active) {
+        hit_idx[j] = bidx;
+        hit_I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f);
+    }
+}
+
+// Shadow queries (isShadow, raytracing.cpp:241-261). With no transparent material the verdict
+// is "some triangle is hit at a distance < FLT_MAX", so lanes stop at their first such hit and
+// the wave leaves the loop once every lane has one.
+template <bool kAnyHit>
+__global__ __launch_bounds__(kBlock) void k_shadow_hit(const TriRec *__restrict__ tris, int nt,
+                                                       const uint32_t *__restrict__ tri_mat,
+                                                       const DevMaterial *__restrict__ mats,
+                                                       const float4 *__restrict__ q_org,
+                                                       const float4 *__restrict__ q_dst,
+                                                       const int32_t *__restrict__ q_count,
+                                                       uint8_t *__restrict__ shadow) {
+    const int n = *q_count;
+    const int base = blockIdx.x * kBlock;
+    if (base >= n) return;
+    const int j = base + threadIdx.x;
+    const bool active = j < n;
+    V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
+    int slot = 0;
+    if (active) {
+        const float4 qo = q_org[j], qd = q_dst[j];
+        o = mk(qo.x, qo.y, qo.z);
+        dir = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);
+        slot = as_int(qo.w);
+    }
+    int bidx = -1;
+    V3 bI = mk(0, 0, 0);
+    closest_hit_loop<kAnyHit>(tris, nt, o, dir, active, bidx, bI);
+    if (active) {
+        uint8_t sh = 0;
+        if (bidx >= 0) sh = mats[tri_mat[bidx]].transparent ? 0 : 1;               // :253-257
+        shadow[slot] = sh;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_intersect_only(const TriRec *__restrict__ tris, int nt,
+                                                           const float4 *__restrict__ q_org,
+                                                           const float4 *__restrict__ q_dst, int n,
+                                                           int32_t *__restrict__ idx, float4 *__restrict__ I) {
+    const int j = blockIdx.x * kBlock + threadIdx.x;
+    if (blockIdx.x * kBlock >= n) return;
+    const bool active = j < n;
+    V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
+    if (active) {
+        const float4 qo = q_org[j], qd = q_dst[j];
+        o = mk(qo.x, qo.y, qo.z);
+        dir = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);
+    }
+    int bidx = -1;
+    V3 bI = mk(0, 0, 0);
+    closest_hit_loop<false>(tris, nt, o, dir, active, bidx, bI);
+    if (active) { idx[j] = bidx; I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f); }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sample generation: main.cpp:377-386 for every sub-sample of the batch's tiles.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool decode_pixel(const FrameGeom &g, int64_t pix, int &x, int &y) {
+    const int tpx = g.tw * g.th;
+    const int tl = static_cast<int>(pix / tpx);
+    const int p = static_cast<int>(pix - static_cast<int64_t>(tl) * tpx);
+    const int tid = g.first + (g.tile0 + tl) * g.stride;
+    const int tx = tid % g.tiles_x, ty = tid / g.tiles_x;
+    x = g.ox + tx * g.tw + (p % g.tw);
+    y = g.oy + ty * g.th + (p / g.tw);
+    return x < g.width && y < g.height && x < g.ox + g.cw && y < g.oy + g.ch && x >= 0 && y >= 0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWork w) {
+    const int spp = g.pfx * g.pfy;
+    const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th * spp;
+    const int64_t s = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    bool valid = false;
+    V3 origin = mk(0, 0, 0), dest = mk(0, 0, 0);
+    if (s < n) {
+        const int64_t pix = s / spp;
+        const int sub = static_cast<int>(s - pix * spp);
+        const int subx = sub / g.pfy, suby = sub - subx * g.pfy;   // subx outer, suby inner (:377-378)
+        int x, y;
+        valid = decode_pixel(g, pix, x, y);
+        if (valid) {
+            const float xscale = 1.0f - (static_cast<float>(static_cast<unsigned>(x)) * static_cast<float>(static_cast<unsigned>(g.pfx)) + static_cast<float>(subx)) / g.divX;  // :380
+            const float yscale = 1.0f - (static_cast<float>(static_cast<unsigned>(y)) * static_cast<float>(static_cast<unsigned>(g.pfy)) + static_cast<float>(suby)) / g.divY;  // :381
+            const V3 o00 = mk(g.corners[0][0], g.corners[0][1], g.corners[0][2]);
+            const V3 d00 = mk(g.corners[1][0], g.corners[1][1], g.corners[1][2]);
+            const V3 o01 = mk(g.corners[2][0], g.corners[2][1], g.corners[2][2]);
+            const V3 d01 = mk(g.corners[3][0], g.corners[3][1], g.corners[3][2]);
+            const V3 o10 = mk(g.corners[4][0], g.corners[4][1], g.corners[4][2]);
+            const V3 d10 = mk(g.corners[5][0], g.corners[5][1], g.corners[5][2]);
+            const V3 o11 = mk(g.corners[6][0], g.corners[6][1], g.corners[6][2]);
+            const V3 d11 = mk(g.corners[7][0], g.corners[7][1], g.corners[7][2]);
+            const float ix = 1 - xscale, iy = 1 - yscale;
+            origin = add(scale(add(scale(o00, xscale), scale(o10, ix)), yscale),
+                         scale(add(scale(o01, xscale), scale(o11, ix)), iy));                     // :383-384
+            dest = add(scale(add(scale(d00, xscale), scale(d10, ix)), yscale),
+                       scale(add(scale(d01, xscale), scale(d11, ix)), iy));                       // :385-386
+        }
+        if (s < w.cap) w.depth[s] = 0;
+    }
+    const int pos = wave_append(&w.counters[0], valid);
+    if (valid) {
+        w.q_org[0][pos] = make_float4(origin.x, origin.y, origin.z, as_float(static_cast<int>(s)));
+        w.q_dst[0][pos] = make_float4(dest.x, dest.y, dest.z, as_float(0));
+    }
+    const unsigned long long m = __ballot(valid);
+    if (__lane_id() == 0 && m) atomicAdd(&w.rays[0], static_cast<unsigned long long>(__popcll(m)));
+}
+
+__global__ __launch_bounds__(kBlock) void k_gen_rays(const float4 *__restrict__ org, const float4 *__restrict__ dst,
+                                                     int32_t n, DevWork w) {
+    const int s = blockIdx.x * kBlock + threadIdx.x;
+    const bool valid = s < n;
+    const int pos = wave_append(&w.counters[0], valid);
+    if (valid) {
+        const float4 o = org[s], d = dst[s];
+        w.q_org[0][pos] = make_float4(o.x, o.y, o.z, as_float(s));
+        w.q_dst[0][pos] = make_float4(d.x, d.y, d.z, as_float(0));
+        w.depth[s] = 0;
+    }
+    const unsigned long long m = __ballot(valid);
+    if (__lane_id() == 0 && m) atomicAdd(&w.rays[0], static_cast<unsigned long long>(__popcll(m)));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Shadow query generation: for each hit query and each light, origin = I + (0.1,0.1,0.1)
+// (raytracing.cpp:246), destination = light position (:248).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_shadow_gen(const ShadeParams p, DevWork w) {
+    const int slot_q = blockIdx.x * kBlock + threadIdx.x;          // (query, light) pair
+    const int L = p.n_lights;
+    const int n = w.counters[p.step];
+    const int j = slot_q / L, l = slot_q - j * L;
+    bool valid = false;
+    float4 so = make_float4(0, 0, 0, 0), sd = so;
+    if (j < n) {
+        if (w.hit_idx[j] >= 0) {
+            const float4 I = w.hit_I[j];
+            so = make_float4(I.x + 0.1f, I.y + 0.1f, I.z + 0.1f, as_float(slot_q));
+            sd = make_float4(p.lights[l][0], p.lights[l][1], p.lights[l][2], 0.0f);
+            valid = true;
+        }
+    }
+    if (blockIdx.x * kBlock >= n * L) return;   // whole block past the end: uniform exit
+    const int pos = wave_append(&w.counters[kMaxStepsCounters + p.step], valid);
+    if (valid) { w.sq_org[pos] = so; w.sq_dst[pos] = sd; }
+    const unsigned long long m = __ballot(valid);
+    if (__lane_id() == 0 && m) atomicAdd(&w.rays[2], static_cast<unsigned long long>(__popcll(m)));
+}
+
+// ---------------------------------------------------------------------------------------------
+// shade (raytracing.cpp:335-368) for one hit, plus the secondary ray it spawns.
+// ---------------------------------------------------------------------------------------------
+struct Secondary {
+    uint32_t state;     // kChildNone / kChildTrace / kChildZero
+    V3 coef;
+    V3 org, dst;
+    int lvl;
+};
+
+// reflection (raytracing.cpp:277-285) + addOffset (:266-271): the traced ray of level `lvl`.
+__device__ __forceinline__ void reflection_ray(V3 ray, V3 p, V3 normal, V3 &point, V3 &dest) {
+    normalize(ray);
+    const V3 R = sub(ray, scale(normal, 2.0f * dot(normal, ray)));
+    point = p;
+    dest = add(p, R);
+    V3 v = sub(dest, point);
+    normalize(v);
+    v = scale(v, 0.01f);
+    point = add(point, v);
+}
+
+__device__ __forceinline__ void offset_point(V3 &point, V3 dest) {   // addOffset
+    V3 v = sub(dest, point);
+    normalize(v);
+    v = scale(v, 0.01f);
+    point = add(point, v);
+}
+
+__global__ __launch_bounds__(kBlock) void k_shade(const DevScene sc, const ShadeParams p, DevWork w) {
+    const int j = blockIdx.x * kBlock + threadIdx.x;
+    const int n = w.counters[p.step];
+    if (blockIdx.x * kBlock >= n) return;
+    const bool active = j < n;
+    Secondary sec;
+    sec.state = kChildNone;
+    int sample = 0;
+    if (active) {
+        const float4 qo = w.q_org[p.step & 1][j], qd = w.q_dst[p.step & 1][j];
+        sample = as_int(qo.w);
+        const int lvl = as_int(qd.w);
+        const int idx = w.hit_idx[j];
+        const int64_t ci = static_cast<int64_t>(p.step) * w.cap + sample;
+        if (idx < 0) {                                                   // trace() miss -> BLACK (:389-391)
+            w.chain_local[ci] = make_float4(0, 0, 0, as_float(kChildNone));
+            w.depth[sample] = static_cast<uint8_t>(p.step + 1);
+        } else {
+            const V3 origin = mk(qo.x, qo.y, qo.z), dest = mk(qd.x, qd.y, qd.z);
+            const V3 ray = sub(dest, origin);                                // :393
+            V3 normal = ld3(sc.normals[idx]);                                // :394 (copy, mutated below)
+            const DevMaterial m = sc.mats[sc.tri_mat[idx]];                  // :396
+            const V3 P = ld3(w.hit_I[j]);
+            const V3 Kd = mk(m.Kd[0], m.Kd[1], m.Kd[2]);
+            const V3 Ka = mk(m.Ka[0], m.Ka[1], m.Ka[2]);
+            const V3 Ks = mk(m.Ks[0], m.Ks[1], m.Ks[2]);
+            const uint32_t f = p.flags;
+            V3 color = mk(0, 0, 0);                                          // :336
+            if ((f & RT_AMBIENT) && (m.flags & RT_HAS_KA)) color = add(color, Ka);   // :337-340
+            for (int l = 0; l < p.n_lights; ++l) {                           // :342
+                const V3 L = mk(p.lights[l][0], p.lights[l][1], p.lights[l][2]);
+                const bool shadowed = (f & RT_SHADOWS) ? (w.shadow[j * p.n_lights + l] != 0) : false;
+                if (shadowed) continue;
+                if ((f & RT_DIFFUSE) && (m.flags & RT_HAS_KD)) {             // diffuseOnly :197-205
+                    V3 diffuse = mk(0, 0, 0);
+                    normalize(normal);
+                    V3 lp = L;
+                    normalize(lp);
+                    diffuse = add(diffuse, scale(Kd, max_std(dot(normal, lp), 0.0f)));
+                    color = add(color, scale(diffuse, m.Tr));                // :349
+                }
+                if ((f & RT_SPECULAR) && (m.flags & RT_HAS_KS) && (m.flags & RT_HAS_NS)) {   // :210-232
+                    V3 spec = mk(0, 0, 0);
+                    V3 Vv = sub(mk(p.cam[0], p.cam[1], p.cam[2]), P);
+                    normalize(normal);
+                    normalize(Vv);
+                    V3 Lv = sub(L, P);
+                    normalize(Lv);
+                    V3 H = add(Vv, Lv);
+                    normalize(H);
+                    float st = max_std(dot(H, normal), 0.0f);
+                    st = spec_powf(st, m.Ns);
+                    spec = add(spec, scale(Ks, st));
+                    color = add(color, scale(spec, m.Tr));                   // :353
+                }
+            }
+            if ((f & RT_REFRACTION) && (m.Tr < 1) && lvl < p.max_lvl) {     // :357-359 -> refraction :290-330
+                const int rl = lvl + 1;
+                V3 r = ray;
+                normalize(r);
+                const float check = dot(r, normal);
+                sec.state = kChildZero;
+                if (check < 0) {
+                    if (check >= kAcosLe2Threshold) {                        // 0 < acosf(check) <= 2
+                        sec.state = kChildTrace; sec.coef = Ks; sec.lvl = rl + 1;
+                        reflection_ray(r, P, normal, sec.org, sec.dst);
+                    } else {
+                        const float nr = 1 / m.Ni;
+                        const float root = 1 - m.powf_nr2 * (1 - glibc_powf2(dot(normal, r), sc.ties, sc.n_ties));
+                        if (root >= 0.0f) {
+                            const float rt = sqrtf(root);
+                            const V3 T = sub(scale(sub(r, scale(normal, dot(normal, r))), nr), scale(normal, rt));
+                            sec.org = P;
+                            sec.dst = add(P, T);
+                            offset_point(sec.org, sec.dst);
+                            sec.state = kChildTrace; sec.lvl = rl + 1;
+                            const float c = 1 - m.Tr;
+                            sec.coef = mk(c, c, c);
+                        }
+                    }
+                } else {
+                    const float nr = m.Ni;
+                    const V3 nn = neg(normal);
+                    const float root = 1 - m.powf_ni2 * (1 - glibc_powf2(dot(nn, r), sc.ties, sc.n_ties));
+                    if (root >= 0.0f) {
+                        const float rt = sqrtf(root);
+                        const V3 T = sub(scale(sub(r, scale(nn, dot(nn, r))), nr), scale(nn, rt));
+                        sec.org = P;
+                        sec.dst = add(P, T);
+                        offset_point(sec.org, sec.dst);
+                        sec.state = kChildTrace; sec.lvl = rl + 1;
+                        const float c = 1 - m.Tr;
+                        sec.coef = mk(c, c, c);
+                    }
+                }
+            } else if ((f & RT_REFLECTION) && lvl < p.max_lvl) {            // :361-363
+                sec.state = kChildTrace; sec.coef = Ks; sec.lvl = lvl + 1;
+                reflection_ray(ray, P, normal, sec.org, sec.dst);
+            }
+            w.chain_local[ci] = make_float4(color.x, color.y, color.z, as_float(static_cast<int>(sec.state)));
+            if (sec.state == kChildTrace) w.chain_coef[ci] = make_float4(sec.coef.x, sec.coef.y, sec.coef.z, 0.0f);
+            else w.depth[sample] = static_cast<uint8_t>(p.step + 1);
+        }
+    }
+    const bool spawn = active && sec.state == kChildTrace;
+    const int pos = wave_append(&w.counters[p.step + 1], spawn);
+    if (spawn) {
+        const int nb = (p.step + 1) & 1;
+        w.q_org[nb][pos] = make_float4(sec.org.x, sec.org.y, sec.org.z, as_float(sample));
+        w.q_dst[nb][pos] = make_float4(sec.dst.x, sec.dst.y, sec.dst.z, as_float(sec.lvl));
+    }
+    const unsigned long long m2 = __ballot(spawn);
+    if (__lane_id() == 0 && m2) atomicAdd(&w.rays[1], static_cast<unsigned long long>(__popcll(m2)));
+}
+
+// Fold one sample's chain back to front: c_k = local_k + coef_k * c_{k+1} (the order in which
+// shade() adds the value returned by the recursive trace(), raytracing.cpp:359,363).
+__device__ __forceinline__ V3 fold_chain(const DevWork &w, int64_t s) {
+    V3 c = mk(0, 0, 0);
+    const int d = w.depth[s];
+    for (int k = d - 1; k >= 0; --k) {
+        const int64_t ci = static_cast<int64_t>(k) * w.cap + s;
+        const float4 L = w.chain_local[ci];
+        const uint32_t st = static_cast<uint32_t>(as_int(L.w));
+        if (st == kChildTrace) {
+            const float4 K = w.chain_coef[ci];
+            c = add(mk(L.x, L.y, L.z), mul(mk(K.x, K.y, K.z), c));
+        } else if (st == kChildZero) {
+            c = add(mk(L.x, L.y, L.z), mk(0.0f, 0.0f, 0.0f));
+        } else {
+            c = mk(L.x, L.y, L.z);
+        }
+    }
+    return c;
+}
+
+// Frame: per pixel, sum sub-samples (subx outer, suby inner), divide by pf^2 (main.cpp:391),
+// clamp (RGBValue, main.cpp:29-41), quantise with truncation (main.cpp:117; NaN -> 0).
+__global__ __launch_bounds__(kBlock) void k_frame(const FrameGeom g, DevWork w, uint8_t *__restrict__ out_u8,
+                                                  float *__restrict__ out_f32) {
+    const int64_t npix = static_cast<int64_t>(g.ntiles) * g.tw * g.th;
+    const int64_t pix = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (pix >= npix) return;
+    int x, y;
+    const bool valid = decode_pixel(g, pix, x, y);
+    const int spp = g.pfx * g.pfy;
+    int64_t o;
+    if (g.out_mode == 0) o = 3 * (static_cast<int64_t>(g.tile0) * g.tw * g.th + pix);
+    else o = 3 * (static_cast<int64_t>(y - g.oy) * g.cw + (x - g.ox));
+    if (!valid) {
+        if (g.out_mode == 0 && out_u8) { out_u8[o] = 0; out_u8[o + 1] = 0; out_u8[o + 2] = 0; }
+        return;
+    }
+    V3 rgb = mk(0, 0, 0);
+    for (int sub = 0; sub < spp; ++sub) rgb = add(rgb, fold_chain(w, pix * spp + sub));
+    const float div = static_cast<float>(spp);
+    rgb = mk(rgb.x / div, rgb.y / div, rgb.z / div);                 // operator/, Vec3D.h:36-38
+    float c[3] = {rgb.x, rgb.y, rgb.z};
+    for (int k = 0; k < 3; ++k) {
+        float v = c[k];
+        if (v > 1) v = 1.0f;
+        if (v < 0) v = 0.0f;
+        if (out_f32) out_f32[o + k] = v;
+        if (out_u8) {
+            const float q = v * 255.0f;
+            out_u8[o + k] = (q == q) ? static_cast<uint8_t>(static_cast<int>(q)) : 0;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_fold_rays(DevWork w, int32_t n, float *__restrict__ rgb) {
+    const int s = blockIdx.x * kBlock + threadIdx.x;
+    if (s >= n) return;
+    const V3 c = fold_chain(w, s);
+    rgb[3 * s] = c.x; rgb[3 * s + 1] = c.y; rgb[3 * s + 2] = c.z;
+}
+
+inline unsigned grid_for(int64_t n) { return static_cast<unsigned>((n + kBlock - 1) / kBlock); }
+
+}  // namespace
+
+void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream) {
+    const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th * g.pfx * g.pfy;
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_gen_primary, dim3(grid_for(n)), dim3(kBlock), 0, stream, g, w);
+}
+
+void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevWork &w, hipStream_t stream) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_gen_rays, dim3(grid_for(n)), dim3(kBlock), 0, stream, org, dst, n, w);
+}
+
+void launch_closest_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
+    if (capacity <= 0) return;
+    hipLaunchKernelGGL(k_closest_hit, dim3(grid_for(capacity)), dim3(kBlock), 0, stream, s.tris, s.nt,
+                       w.q_org[step & 1], w.q_dst[step & 1], &w.counters[step], w.hit_idx, w.hit_I);
+}
+
+void launch_shadow_gen(const DevScene &, const DevWork &w, const ShadeParams &p, int64_t capacity, hipStream_t stream) {
+    const int64_t n = capacity * p.n_lights;
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_shadow_gen, dim3(grid_for(n)), dim3(kBlock), 0, stream, p, w);
+}
+
+void launch_shadow_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
+    if (capacity <= 0) return;
+    if (s.any_transparent)
+        hipLaunchKernelGGL(k_shadow_hit<false>, dim3(grid_for(capacity)), dim3(kBlock), 0, stream, s.tris, s.nt,
+                           s.tri_mat, s.mats, w.sq_org, w.sq_dst, &w.counters[kMaxStepsCounters + step], w.shadow);
+    else
+        hipLaunchKernelGGL(k_shadow_hit<true>, dim3(grid_for(capacity)), dim3(kBlock), 0, stream, s.tris, s.nt,
+                           s.tri_mat, s.mats, w.sq_org, w.sq_dst, &w.counters[kMaxStepsCounters + step], w.shadow);
+}
+
+void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int64_t capacity, hipStream_t stream) {
+    if (capacity <= 0) return;
+    hipLaunchKernelGGL(k_shade, dim3(grid_for(capacity)), dim3(kBlock), 0, stream, s, p, w);
+}
+
+void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream) {
+    const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th;
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_frame, dim3(grid_for(n)), dim3(kBlock), 0, stream, g, w, out_u8, out_f32);
+}
+
+void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t stream) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_fold_rays, dim3(grid_for(n)), dim3(kBlock), 0, stream, w, n, rgb);
+}
+
+void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *dst, int32_t n, int32_t *idx,
+                           float4 *I, hipStream_t stream) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_intersect_only, dim3(grid_for(n)), dim3(kBlock), 0, stream, s.tris, s.nt, org, dst, n, idx, I);
+}
+
+}  // namespace rt

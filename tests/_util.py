@@ -1,0 +1,72 @@
+"""Shared helpers for the test suite: fixture inputs and golden outputs."""
+from __future__ import annotations
+
+import gzip
+import json
+import os
+import shutil
+import sys
+
+import numpy as np
+
+TESTS = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(TESTS)
+GOLDEN = os.path.join(TESTS, "golden")
+MODELS = os.path.join(GOLDEN, "models")
+for p in (ROOT, os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+from raytracert_amd import scenes  # noqa: E402
+
+
+def materialize_models(dst: str) -> str:
+    """Decompress the reference's model inputs (CG_Project/*.obj/*.mtl, kept gzip'd as data
+    fixtures) into dst, preserving the Models/ sub-directory. Returns dst."""
+    for dirpath, _, files in os.walk(MODELS):
+        rel = os.path.relpath(dirpath, MODELS)
+        out_dir = os.path.join(dst, rel) if rel != "." else dst
+        os.makedirs(out_dir, exist_ok=True)
+        for f in files:
+            if f.endswith(".gz"):
+                out = os.path.join(out_dir, f[:-3])
+                if not os.path.exists(out):
+                    with gzip.open(os.path.join(dirpath, f), "rb") as src, open(out, "wb") as o:
+                        shutil.copyfileobj(src, o)
+    return dst
+
+
+def scene_path(spec: str, workdir: str) -> str:
+    """spec = 'ref:<file under CG_Project>' or 'syn:<GridSpec name in raytracert_amd.scenes>'."""
+    kind, name = spec.split(":", 1)
+    if kind == "ref":
+        materialize_models(workdir)
+        return os.path.join(workdir, name)
+    if kind == "syn":
+        return scenes.write_sphere_grid(getattr(scenes, name), workdir, name.lower())
+    raise ValueError(spec)
+
+
+def golden_index() -> dict:
+    with open(os.path.join(GOLDEN, "index.json")) as f:
+        return json.load(f)
+
+
+def survey_pins() -> dict:
+    with open(os.path.join(GOLDEN, "survey_pins.json")) as f:
+        return json.load(f)
+
+
+def read_ppm(path: str) -> np.ndarray:
+    with open(path, "rb") as f:
+        data = f.read()
+    parts = data.split(b"\n", 3)
+    assert parts[0] == b"P6" and parts[2] == b"255", "not a P6/255 PPM"
+    w, h = (int(v) for v in parts[1].split())
+    return np.frombuffer(parts[3], np.uint8).reshape(h, w, 3)
+
+
+def golden(name: str):
+    u8 = read_ppm(os.path.join(GOLDEN, name + ".ppm"))
+    f32 = np.load(os.path.join(GOLDEN, name + ".rgb_f32.npy"), allow_pickle=False)
+    return u8, f32

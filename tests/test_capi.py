@@ -1,0 +1,77 @@
+"""The C-ABI boundary without a GPU: the library loads, exports every symbol the header
+declares, and its host-side entries behave (errors, camera, PPM writer)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle as O
+import raytracert_amd as R
+from raytracert_amd import _capi
+from _util import survey_pins, read_ppm
+
+
+def test_library_exports_every_header_symbol():
+    lib = _capi.lib()
+    syms = _capi.header_symbols()
+    assert len(syms) >= 17
+    for s in syms:
+        assert hasattr(lib, s), s
+    # the Python binding declares a signature for every exported entry
+    assert set(syms) == set(_capi._SIGNATURES)
+
+
+def test_struct_layouts_match_header():
+    assert C.sizeof(_capi.RtParams) == 4 * 8 + 16 * 12 + 12 + 8 * 12
+    assert C.sizeof(_capi.RtMaterial) == 4 * 14
+    assert C.sizeof(_capi.RtParams) == C.sizeof(O.OraParams)
+
+
+def test_default_corners_bitwise_equal_oracle_and_pins():
+    for w, h in [(64, 64), (800, 600), (1920, 1080), (3840, 2160), (48, 27)]:
+        a = R.default_corners(w, h)
+        b = O.default_corners(w, h)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    pins = survey_pins()["corners_1920x1080"]
+    c = R.default_corners(1920, 1080)
+    np.testing.assert_allclose(c[0], pins["o00"], atol=5e-7, rtol=0)
+    np.testing.assert_allclose(c[7], pins["d11"], atol=5e-7, rtol=0)
+
+
+def test_write_ppm_roundtrip(tmp_path):
+    img = (np.arange(5 * 7 * 3) % 256).astype(np.uint8).reshape(5, 7, 3)
+    p = str(tmp_path / "x.ppm")
+    R.write_ppm(p, img)
+    assert open(p, "rb").read(11) == b"P6\n7 5\n255\n"
+    assert np.array_equal(read_ppm(p), img)
+
+
+def test_errors_are_codes_with_messages(tmp_path):
+    with pytest.raises(R.RtError) as ei:
+        R.default_corners(0, 10)
+    assert ei.value.code == _capi.RT_E_ARG
+    with pytest.raises(R.RtError) as ei:
+        R.write_ppm(str(tmp_path / "nodir" / "x.ppm"), np.zeros((2, 2, 3), np.uint8))
+    assert ei.value.code == _capi.RT_E_IO
+
+
+def test_host_only_scene_refuses_render(tmp_path):
+    p = tmp_path / "t.obj"
+    p.write_text("v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 3\n")
+    s = R.Scene.load(str(p), device=R.RT_HOST_ONLY)
+    with pytest.raises(R.RtError) as ei:
+        s.render(R.RenderParams(width=4, height=4, pf=1, max_lvl=0))
+    assert ei.value.code == _capi.RT_E_NODEV
+    with pytest.raises(R.RtError):
+        s.intersect_mesh([[0, 0, 1]], [[0, 0, -1]])
+    assert s.get_material(0)["Kd"] == (0.5, 0.5, 0.5)   # default material (mesh.cpp:108-117)
+
+
+def test_scene_create_validates_indices():
+    with pytest.raises(R.RtError) as ei:
+        R.Scene.create([[0, 0, 0]], [[0, 0, 1]], [0], [dict(Kd=(1, 1, 1), flags=1)], device=R.RT_HOST_ONLY)
+    assert ei.value.code == _capi.RT_E_PARSE
+    s = R.Scene.create([[0, 0, 0], [1, 0, 0], [0, 1, 0]], [[0, 1, 2]], [0], [dict(Kd=(1, 1, 1), flags=1)],
+                       device=R.RT_HOST_ONLY)
+    assert s.counts() == (3, 1, 1)
+    assert s.export()["normals"].tolist() == [[0.0, 0.0, 1.0]]

@@ -1,0 +1,88 @@
+"""librtamd's OBJ/MTL loader (host-only scenes, no GPU) against the oracle's restatement of
+Mesh::loadMesh / loadMtl (CG_Project/mesh.cpp:95-460): identical vertices, triangle lists,
+material table and face normals, bit for bit."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+import raytracert_amd as R
+from _util import scene_path
+
+
+def _same(a, b):
+    if a.dtype == np.float32:
+        return np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    return np.array_equal(a, b)
+
+
+def _compare(path):
+    e = R.Scene.load(path, device=R.RT_HOST_ONLY).export()
+    o = O.OracleScene(path).export()
+    for k in ("vertices", "triangles", "tri_mat", "normals"):
+        assert _same(e[k], o[k]), k
+    assert e["materials"] == o["materials"]
+    return e
+
+
+@pytest.mark.parametrize("spec", ["ref:cube.obj", "ref:dodgeColorTest.obj", "ref:Models/shadow_test.obj",
+                                  "syn:F3", "syn:F4", "syn:C4"])
+def test_loader_matches_oracle(spec, workdir):
+    e = _compare(scene_path(spec, workdir))
+    assert len(e["materials"]) >= 2   # default material + the MTL's
+
+
+def test_dodge_counts(workdir):
+    e = _compare(scene_path("ref:dodgeColorTest.obj", workdir))
+    assert len(e["vertices"]) == 8373 and len(e["triangles"]) == 16311   # 6 quads fan-split
+
+
+def test_cube_materials_unset_tr_reads_zero(workdir):
+    """cube.mtl sets no d/Tr: Tr reads 0, so the lit terms vanish and the cube
+    renders black."""
+    e = _compare(scene_path("ref:cube.obj", workdir))
+    for m in e["materials"][1:]:
+        assert m["Tr"] == 0.0 and not (m["flags"] & 0x20)
+
+
+def _write(d, name, text):
+    with open(os.path.join(d, name), "w", newline="") as f:
+        f.write(text)
+    return os.path.join(d, name)
+
+
+def test_quirks(tmp_path):
+    d = str(tmp_path)
+    # MTL: second block has no Ks -> inherits the first block's Ks value but not its flag;
+    # a block without a blank line before the next newmtl is overwritten (no commit);
+    # d and Tr both set Tr; CRLF lines; last block committed at EOF without a trailing newline.
+    _write(d, "q.mtl", "newmtl A\r\nKd 1 0 0\r\nKs 0.25 0.5 0.75\r\nNs 10\r\n\r\n"
+                       "newmtl B\nKd 0 1 0\nd 0.5\n\nnewmtl C\nKd 0 0 1\nnewmtl D\nKa 0.1 0.2 0.3\nTr 0.75")
+    # OBJ: quad -> fan; 'f' with v/t/n and v//n tokens; unknown material -> default 0;
+    # a 'v' line missing z keeps the previous z; a face referencing a missing vertex is dropped.
+    _write(d, "q.obj", "mtllib q.mtl\nv 0 0 1\nv 1 0\nv 1 1 2\nv 0 1 3\n"
+                       "usemtl A\nf 1/1/1 2/2/2 3/3/3 4/4/4\nusemtl B\nf 1//1 3//1 4//1\n"
+                       "usemtl Nope\nf 1 2 3\nusemtl D\nf 2 3 4\nf 1 2 9\n")
+    e = _compare(os.path.join(d, "q.obj"))
+    assert e["vertices"][1].tolist() == [1.0, 0.0, 1.0]
+    assert e["triangles"].tolist() == [[0, 1, 2], [0, 2, 3], [0, 2, 3], [0, 1, 2], [1, 2, 3]]
+    names = ["default", "A", "B", "D"]
+    assert len(e["materials"]) == len(names)
+    assert e["tri_mat"].tolist() == [1, 1, 2, 0, 3]
+    B = e["materials"][2]
+    assert B["Tr"] == 0.5 and B["Ks"] == (0.25, 0.5, 0.75) and not (B["flags"] & 0x4)
+    D = e["materials"][3]   # C's Kd was overwritten by D's block: D carries Kd (0,0,1) and Tr .75
+    assert D["Kd"] == (0.0, 0.0, 1.0) and D["Tr"] == 0.75
+
+
+def test_missing_obj_is_an_error():
+    with pytest.raises(R.RtError) as ei:
+        R.Scene.load("/nonexistent/model.obj", device=R.RT_HOST_ONLY)
+    assert ei.value.code == -1
+
+
+def test_missing_mtl_warns_and_uses_default(tmp_path):
+    p = _write(str(tmp_path), "m.obj", "mtllib nothere.mtl\nv 0 0 0\nv 1 0 0\nv 0 1 0\nusemtl X\nf 1 2 3\n")
+    e = _compare(p)
+    assert e["tri_mat"].tolist() == [0] and len(e["materials"]) == 1
