@@ -96,6 +96,13 @@ def lib() -> C.CDLL:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: build it with `make -C raytracert_amd` "
                               "(or __graft_entry__.build()); there is no CPU fallback")
+        # torch bundles its own libamdhip64.so.7 / libhsa-runtime64; if it is loaded after
+        # librtamd.so (which resolves /opt/rocm's), the process holds two HIP runtimes and torch
+        # finds no GPU. Loading torch first makes librtamd bind to the already-loaded runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (args, res) in _SIGNATURES.items():
             fn = getattr(L, name)

@@ -95,37 +95,64 @@ __device__ __forceinline__ int wave_append(int32_t *counter, bool pred) {
 // triangle loop is wave-uniform, so each 64-byte record is fetched with scalar loads and the VALU
 // reads it from SGPRs (no VGPR/LDS copy).
 // ---------------------------------------------------------------------------------------------
+// Forces every SGPR of a scalar-loaded record to be resident (s_waitcnt) at this point, and
+// keeps later loads below it, so the next record's s_load overlaps this record's arithmetic.
+__device__ __forceinline__ void sgpr_fence(const TriRec &T) {
+    asm volatile("" ::"s"(T.t0[0]), "s"(T.t0[1]), "s"(T.t0[2]), "s"(T.uu), "s"(T.u[0]), "s"(T.u[1]), "s"(T.u[2]),
+                 "s"(T.uv), "s"(T.v[0]), "s"(T.v[1]), "s"(T.v[2]), "s"(T.vv), "s"(T.n[0]), "s"(T.n[1]), "s"(T.n[2]),
+                 "s"(T.D)
+                 : "memory");
+}
+
+// One rayIntersectTriangle + intersectMesh update (raytracing.cpp:106-154, :180-187).
+template <bool kAnyHit>
+__device__ __forceinline__ void test_triangle(const TriRec &T, int t, V3 o, V3 dir, float &best, int &bidx, V3 &bI,
+                                              bool &done) {
+    if (kAnyHit && done) return;
+    const V3 w0 = mk(o.x - T.t0[0], o.y - T.t0[1], o.z - T.t0[2]);
+    const float b = T.n[0] * dir.x + T.n[1] * dir.y + T.n[2] * dir.z;          // :113
+    const float a = -(T.n[0] * w0.x + T.n[1] * w0.y + T.n[2] * w0.z);          // :114
+    if (fabsf(b) < 0.00001f) return;                                            // :115
+    const float r = a / b;                                                      // :124
+    if (r < 0) return;                                                          // :125
+    const V3 I = mk(o.x + dir.x * r, o.y + dir.y * r, o.z + dir.z * r);         // :130
+    const V3 w = mk(I.x - T.t0[0], I.y - T.t0[1], I.z - T.t0[2]);               // :137
+    const float wu = w.x * T.u[0] + w.y * T.u[1] + w.z * T.u[2];                 // :138
+    const float wv = w.x * T.v[0] + w.y * T.v[1] + w.z * T.v[2];                 // :139
+    const float s = (T.uv * wv - T.vv * wu) / T.D;                              // :144
+    if (s < 0 || s > 1) return;                                                 // :145
+    const float tt = (T.uv * wu - T.uu * wv) / T.D;                             // :148
+    if (tt < 0 || (s + tt) > 1) return;                                         // :149
+    const V3 e = sub(o, I);                                                     // distance, Vec3D.h:199-202
+    const float dist = sqrtf(dot(e, e));
+    if (dist < best) {                                                          // :183
+        best = dist; bidx = t; bI = I;
+        if (kAnyHit) done = true;
+    }
+}
+
+// Scalar-load pipeline: records A and B alternate; each is fenced (s_waitcnt) before the next
+// record's s_load is issued, so one load is always in flight behind the arithmetic.
 template <bool kAnyHit>
 __device__ __forceinline__ void closest_hit_loop(const TriRec *__restrict__ tris, int nt, V3 o, V3 dir, bool active,
                                                  int &bidx, V3 &bI) {
     float best = FLT_MAX;
     bool done = !active;
-    for (int t = 0; t < nt; ++t) {
-        if (kAnyHit) {
-            if ((t & 15) == 0 && __all(done)) break;
-            if (done) continue;
-        }
-        const TriRec T = tris[t];
-        const V3 w0 = mk(o.x - T.t0[0], o.y - T.t0[1], o.z - T.t0[2]);
-        const float b = T.n[0] * dir.x + T.n[1] * dir.y + T.n[2] * dir.z;          // :113
-        const float a = -(T.n[0] * w0.x + T.n[1] * w0.y + T.n[2] * w0.z);          // :114
-        if (fabsf(b) < 0.00001f) continue;                                          // :115
-        const float r = a / b;                                                      // :124
-        if (r < 0) continue;                                                        // :125
-        const V3 I = mk(o.x + dir.x * r, o.y + dir.y * r, o.z + dir.z * r);         // :130
-        const V3 w = mk(I.x - T.t0[0], I.y - T.t0[1], I.z - T.t0[2]);               // :137
-        const float wu = w.x * T.u[0] + w.y * T.u[1] + w.z * T.u[2];                 // :138
-        const float wv = w.x * T.v[0] + w.y * T.v[1] + w.z * T.v[2];                 // :139
-        const float s = (T.uv * wv - T.vv * wu) / T.D;                              // :144
-        if (s < 0 || s > 1) continue;                                               // :145
-        const float tt = (T.uv * wu - T.uu * wv) / T.D;                             // :148
-        if (tt < 0 || (s + tt) > 1) continue;                                       // :149
-        const V3 e = sub(o, I);                                                     // distance, Vec3D.h:199-202
-        const float dist = sqrtf(dot(e, e));
-        if (dist < best) {                                                          // :183
-            best = dist; bidx = t; bI = I;
-            if (kAnyHit) done = true;
-        }
+    if (nt <= 0) return;
+    TriRec A = tris[0];
+    int t = 0;
+    for (; t + 1 < nt; t += 2) {
+        if (kAnyHit && (t & 15) == 0 && __all(done)) return;
+        sgpr_fence(A);
+        const TriRec B = tris[t + 1];
+        test_triangle<kAnyHit>(A, t, o, dir, best, bidx, bI, done);
+        sgpr_fence(B);
+        A = tris[min(t + 2, nt - 1)];
+        test_triangle<kAnyHit>(B, t + 1, o, dir, best, bidx, bI, done);
+    }
+    if (t < nt) {
+        sgpr_fence(A);
+        test_triangle<kAnyHit>(A, t, o, dir, best, bidx, bI, done);
     }
 }
 
