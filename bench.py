@@ -161,6 +161,7 @@ def main():
         # algorithmic HBM bytes of the closest-hit kernel: each wave streams every 64-B triangle
         # record once (scalar loads) and reads/writes its 64 queries (32 B in, 20 B out each)
         ch_bytes = ch_tests / 64.0 * 64.0 + (ch_tests / max(nt, 1)) * 52.0
+        traffic, traffic_src = pmc_traffic("k_closest_hit")
         result = {
             "metric": METRIC,
             "value": round(value, 4),
@@ -192,7 +193,9 @@ def main():
                 "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "bytes/launch (PMC: 2*FETCH_SIZE + WRITE_SIZE)",
+                "traffic_source": traffic_src,
                 "launches": ch_launches,
                 "avg_launch_ms": round(ch_ms / max(ch_launches, 1), 3),
                 "tests_per_launch": round(ch_tests / max(ch_launches, 1)),
@@ -220,6 +223,22 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*_pmc.json,
+    written by tools/pmc_summary.py from separate rocprofv3 --pmc passes of this bench command)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc.json")), key=os.path.getmtime)
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        if k and "traffic_bytes_per_launch" in k:
+            return k["traffic_bytes_per_launch"], os.path.relpath(f, HERE)
+    return None, None
 
 
 def cpu_baseline(obj, params, gpu_frame, layout, args):
