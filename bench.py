@@ -29,6 +29,7 @@ sys.path.insert(0, HERE)
 
 METRIC = "Mrays/s + wall-clock per frame at 1920×1080, 100k-tri OBJ"
 FLOP_PER_TEST = 37            # fp32 ops of rayIntersectTriangle's dominant path
+FLOP_PER_NODE = 52            # BVH node visit: 2 slab tests (6 sub + 6 mul + 12 min/max each) + 2 distance culls
 FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector (= FP32 matrix) peak
 HBM_PEAK_GBS = 8000.0
 WIDTH, HEIGHT, PF, MAX_LVL = 1920, 1080, 1, 3
@@ -47,6 +48,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=1, help="steps re-run with HIP events for the roofline")
     ap.add_argument("--ppm", default="", help="write the first frame to this PPM (rank 0)")
+    ap.add_argument("--accel", choices=("bvh", "brute_force"), default="bvh")
+    ap.add_argument("--no-bf-roofline", action="store_true", help="skip the brute-force kernel's roofline frame")
     return ap.parse_args()
 
 
@@ -81,7 +84,9 @@ def main():
     t_gen = time.time() - t_gen
     t_load = time.time()
     scene = R.Scene.load(obj, device=local_rank)
+    scene.set_accel(args.accel)
     t_load = time.time() - t_load
+    bvh_info = scene.bvh_info() if args.accel == "bvh" else None
     nv, nt, nm = scene.counts()
     params = R.RenderParams(width=WIDTH, height=HEIGHT, pf=PF, max_lvl=MAX_LVL, lights=LIGHTS)
     cparams = params.to_c()
@@ -142,26 +147,51 @@ def main():
     elapsed = float(el.item())
 
     # ---- kernel timing for the roofline (HIP events on the scene's launch stream) ----
-    scene.reset_stats()
-    scene.set_profiling(True)
-    for _ in range(max(args.profile_steps, 1)):
-        render_shard()
-    torch.cuda.synchronize(dev)
-    scene.set_profiling(False)
-    ch_launches, ch_ms, ch_tests = scene.kernel_stats(KERNEL_CLOSEST_HIT)
-    sh_launches, sh_ms, sh_tests = scene.kernel_stats(KERNEL_SHADOW)
-    _, shade_ms, _ = scene.kernel_stats(KERNEL_SHADE)
-    _, frame_ms, _ = scene.kernel_stats(KERNEL_FRAME)
+    def profile(steps):
+        scene.reset_stats()
+        scene.set_profiling(True)
+        for _ in range(max(steps, 1)):
+            render_shard()
+        torch.cuda.synchronize(dev)
+        scene.set_profiling(False)
+        st = {k: scene.kernel_stats(k) for k in (KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME)}
+        work = scene.work_stats(KERNEL_CLOSEST_HIT) if scene.accel() == "bvh" else (0.0, 0.0)
+        return st, work
+
+    stats, (bvh_tests, bvh_visits) = profile(args.profile_steps)
+    ch_launches, ch_ms, ch_tests = stats[KERNEL_CLOSEST_HIT]
+    sh_launches, sh_ms, sh_tests = stats[KERNEL_SHADOW]
+    _, shade_ms, _ = stats[KERNEL_SHADE]
+    _, frame_ms, _ = stats[KERNEL_FRAME]
+    bf = None
+    if args.accel == "bvh" and not args.no_bf_roofline and rank == 0:
+        scene.set_accel("brute_force")
+        bst, _ = profile(1)
+        scene.set_accel("bvh")
+        l, ms, tests = bst[KERNEL_CLOSEST_HIT]
+        bf = {"kernel": "k_closest_hit (brute force, --accel brute_force)", "bound": "valu",
+              "achieved": round(tests * FLOP_PER_TEST / (ms / 1e3) / 1e12, 3), "peak": FP32_PEAK_TFLOPS,
+              "unit": "TFLOP/s", "frac": round(tests * FLOP_PER_TEST / (ms / 1e3) / 1e12 / FP32_PEAK_TFLOPS, 4),
+              "launches": l, "avg_launch_ms": round(ms / max(l, 1), 3), "frame_closest_hit_ms": round(ms, 3)}
 
     result = None
     if rank == 0:
         total_rays = rays_per_step * args.steps
         value = total_rays / elapsed / 1e6
-        achieved = ch_tests * FLOP_PER_TEST / (ch_ms / 1e3) / 1e12 if ch_ms > 0 else 0.0
-        # algorithmic HBM bytes of the closest-hit kernel: each wave streams every 64-B triangle
-        # record once (scalar loads) and reads/writes its 64 queries (32 B in, 20 B out each)
-        ch_bytes = ch_tests / 64.0 * 64.0 + (ch_tests / max(nt, 1)) * 52.0
-        traffic, traffic_src = pmc_traffic("k_closest_hit")
+        queries = ch_tests / max(nt, 1)
+        if args.accel == "bvh":
+            # work actually done: triangle tests + node visits (device counters)
+            kname = "k_bvh_closest_hit"
+            flops = bvh_tests * FLOP_PER_TEST + bvh_visits * FLOP_PER_NODE
+            # per query: 32 B in + 20 B out, and 64 B per node visit and per triangle test (L2-served)
+            ch_bytes = queries * 52.0 + (bvh_visits + bvh_tests) * 64.0
+        else:
+            kname = "k_closest_hit"
+            flops = ch_tests * FLOP_PER_TEST
+            # each wave streams every 64-B triangle record once (scalar loads); queries 52 B each
+            ch_bytes = ch_tests / 64.0 * 64.0 + queries * 52.0
+        achieved = flops / (ch_ms / 1e3) / 1e12 if ch_ms > 0 else 0.0
+        traffic, traffic_src = pmc_traffic(kname)
         result = {
             "metric": METRIC,
             "value": round(value, 4),
@@ -187,7 +217,7 @@ def main():
                 "scene_load_s": round(t_load, 3), "scene_gen_s": round(t_gen, 3),
             },
             "roofline": {
-                "kernel": "k_closest_hit (primary + secondary queries, brute force)",
+                "kernel": f"{kname} (primary + secondary queries, accel={args.accel})",
                 "bound": "valu",
                 "achieved": round(achieved, 3),
                 "peak": FP32_PEAK_TFLOPS,
@@ -198,8 +228,12 @@ def main():
                 "traffic_source": traffic_src,
                 "launches": ch_launches,
                 "avg_launch_ms": round(ch_ms / max(ch_launches, 1), 3),
-                "tests_per_launch": round(ch_tests / max(ch_launches, 1)),
+                "queries_per_launch": round(queries / max(ch_launches, 1)),
+                "tests_per_launch": round((bvh_tests if args.accel == "bvh" else ch_tests) / max(ch_launches, 1)),
+                "node_visits_per_launch": round(bvh_visits / max(ch_launches, 1)) if args.accel == "bvh" else 0,
                 "flop_per_test": FLOP_PER_TEST,
+                "flop_per_node_visit": FLOP_PER_NODE,
+                "bruteforce_equivalent_TFLOPs": round(ch_tests * FLOP_PER_TEST / (ch_ms / 1e3) / 1e12, 3) if ch_ms > 0 else None,
                 "hbm_algorithmic_GBps": round(ch_bytes / (ch_ms / 1e3) / 1e9, 2) if ch_ms > 0 else None,
                 "hbm_peak_GBps": HBM_PEAK_GBS,
             },
@@ -209,6 +243,8 @@ def main():
                 "shade": round(shade_ms / max(args.profile_steps, 1), 3),
                 "frame": round(frame_ms / max(args.profile_steps, 1), 3),
             },
+            "roofline_bruteforce": bf,
+            "accel": {"mode": args.accel, "bvh": bvh_info},
             "cpu_baseline": None,
         }
         if args.ppm and frames is not None:

@@ -137,6 +137,24 @@ int rt_default_corners(int32_t width, int32_t height, float corners[8][3]);
 /* Image::writeImage: "P6\n%i %i\n255\n" + w*h*3 bytes. */
 int rt_write_ppm(const char *path, int32_t width, int32_t height, const uint8_t *rgb_u8);
 
+/* ---- acceleration ------------------------------------------------------ */
+/* The reference loops over every triangle for every ray (raytracing.cpp:174-189) and leaves its
+ * KD-tree commented out (:167-172). RT_ACCEL_BVH visits only triangles whose padded acceptance
+ * box the ray can reach; results (index, hit point, every output byte) are identical to
+ * RT_ACCEL_BRUTE_FORCE by construction. Default: RT_ACCEL_BVH. */
+#define RT_ACCEL_BRUTE_FORCE 0
+#define RT_ACCEL_BVH         1
+int rt_scene_set_accel(rt_scene *scene, int32_t mode);
+int rt_scene_get_accel(const rt_scene *scene, int32_t *mode);
+/* info[0] inner nodes, [1] depth, [2] always-tested (ill-conditioned) triangles, [3] never-accepted
+ * (degenerate) triangles, [4] triangles in leaves. Builds the BVH on demand. */
+int rt_scene_bvh_info(rt_scene *scene, int32_t info[5]);
+/* Host-side structural check of the built BVH (containment, coverage, depth bound). */
+int rt_scene_bvh_validate(rt_scene *scene);
+/* The padded acceptance box of one triangle T = {T0, T1, T2} (9 floats), as the BVH uses it.
+ * Returns 0 (box written), 1 (ill-conditioned: tested by every query) or 2 (never accepted). */
+int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
+
 /* ---- measurement ---------------------------------------------------------------------- */
 /* Kernel kinds for rt_kernel_stats. */
 #define RT_KERNEL_CLOSEST_HIT 0   /* closest-hit over all triangles (primary + secondary queries) */
@@ -150,6 +168,9 @@ int rt_set_profiling(rt_scene *scene, int32_t enabled);
 /* launches, summed milliseconds, and summed ray-triangle tests (closest-hit/shadow kinds). */
 int rt_kernel_stats(rt_scene *scene, int32_t kind, uint64_t *launches, double *total_ms, double *tests);
 int rt_reset_stats(rt_scene *scene);
+/* Ray-triangle tests and BVH node visits executed by the BVH kernels of `kind`
+ * (RT_KERNEL_CLOSEST_HIT or RT_KERNEL_SHADOW) since the last reset (synchronises the device). */
+int rt_work_stats(rt_scene *scene, int32_t kind, double *tests, double *node_visits);
 
 #ifdef __cplusplus
 }

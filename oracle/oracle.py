@@ -53,6 +53,7 @@ def lib():
         L.ora_export.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.ora_ray_intersect_triangle.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.ora_ray_intersect_triangle.restype = C.c_int
+        L.ora_ray_intersect_triangle_batch.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]
         L.ora_intersect_mesh.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.ora_intersect_mesh.restype = C.c_int
         L.ora_perform_ray_tracing.argtypes = [C.c_void_p, C.POINTER(OraParams), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -155,3 +156,14 @@ def ray_intersect_triangle(R, T):
     I = np.zeros(3, np.float32)
     hit = lib().ora_ray_intersect_triangle(_ptr(R), _ptr(T), _ptr(I))
     return bool(hit), I
+
+
+def ray_intersect_triangle_batch(R, T):
+    """R: [n, 2, 3] (origin, dest) rays against one triangle T [3, 3] -> (hit[n] bool, I[n, 3])."""
+    R = np.ascontiguousarray(R, np.float32).reshape(-1, 6)
+    T = np.ascontiguousarray(T, np.float32).reshape(9)
+    n = len(R)
+    hit = np.zeros(n, np.uint8)
+    I = np.zeros((n, 3), np.float32)
+    lib().ora_ray_intersect_triangle_batch(_ptr(R), n, _ptr(T), _ptr(hit), _ptr(I))
+    return hit.astype(bool), I

@@ -532,6 +532,10 @@ int ora_ray_intersect_triangle(const float R[6], const float T[9], float I[3]) {
     return hit;
 }
 
+void ora_ray_intersect_triangle_batch(const float *R, int32_t n, const float T[9], uint8_t *hit, float *I) {
+    for (int32_t i = 0; i < n; i++) hit[i] = (uint8_t)ora_ray_intersect_triangle(R + 6 * i, T, I + 3 * i);
+}
+
 int ora_intersect_mesh(const ora_scene *s, const float origin[3], const float dest[3], float I[3]) {
     vec3 out;
     int idx = intersect_mesh(s, V(origin[0], origin[1], origin[2]), V(dest[0], dest[1], dest[2]), &out);

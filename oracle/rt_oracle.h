@@ -71,6 +71,8 @@ void ora_export(const ora_scene *s, float *vertices, uint32_t *tri_v, uint32_t *
 
 /* rayIntersectTriangle (raytracing.cpp:99-154): R = {origin, dest}, T = 3 vertices. */
 int ora_ray_intersect_triangle(const float R[6], const float T[9], float I[3]);
+/* rayIntersectTriangle for n rays R[6n] against one triangle: hit[n] (0/1), I[3n]. */
+void ora_ray_intersect_triangle_batch(const float *R, int32_t n, const float T[9], uint8_t *hit, float *I);
 /* intersectMesh (raytracing.cpp:161-192). Returns triangle index or -1. */
 int ora_intersect_mesh(const ora_scene *s, const float origin[3], const float dest[3], float I[3]);
 /* performRayTracing (raytracing.cpp:410-416). counts (may be NULL): primary, secondary, shadow queries. */

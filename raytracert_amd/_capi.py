@@ -29,6 +29,7 @@ ALL_FEATURES = 0x3F
 HAS_KD, HAS_KA, HAS_KS, HAS_NS, HAS_NI, HAS_TR, HAS_ILLUM = (1 << i for i in range(7))
 
 KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME = range(4)
+ACCEL_BRUTE_FORCE, ACCEL_BVH = 0, 1
 
 
 class RtParams(C.Structure):
@@ -77,6 +78,12 @@ _SIGNATURES = {
     "rt_set_profiling": ([_VP, C.c_int32], C.c_int),
     "rt_kernel_stats": ([_VP, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.POINTER(C.c_double)], C.c_int),
     "rt_reset_stats": ([_VP], C.c_int),
+    "rt_work_stats": ([_VP, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double)], C.c_int),
+    "rt_scene_set_accel": ([_VP, C.c_int32], C.c_int),
+    "rt_scene_get_accel": ([_VP, C.POINTER(C.c_int32)], C.c_int),
+    "rt_scene_bvh_info": ([_VP, _VP], C.c_int),
+    "rt_scene_bvh_validate": ([_VP], C.c_int),
+    "rt_bvh_acceptance_box": ([_VP, _VP, _VP], C.c_int),
 }
 
 _lib = None

@@ -192,6 +192,26 @@ class Scene:
                                            C.byref(n_tiles), _ptr(counts)))
         return n_tiles.value, counts
 
+    # -- acceleration ------------------------------------------------------------------------
+    def set_accel(self, mode) -> None:
+        """'bvh' / 'brute_force' (or RT_ACCEL_* ints). Results are identical either way."""
+        m = {"bvh": _capi.ACCEL_BVH, "brute_force": _capi.ACCEL_BRUTE_FORCE}.get(mode, mode)
+        check(lib().rt_scene_set_accel(self._h, int(m)))
+
+    def accel(self) -> str:
+        m = C.c_int32()
+        check(lib().rt_scene_get_accel(self._h, C.byref(m)))
+        return "bvh" if m.value == _capi.ACCEL_BVH else "brute_force"
+
+    def bvh_info(self) -> dict:
+        info = np.zeros(5, np.int32)
+        check(lib().rt_scene_bvh_info(self._h, _ptr(info)))
+        return dict(nodes=int(info[0]), depth=int(info[1]), always=int(info[2]), never=int(info[3]),
+                    leaf_triangles=int(info[4]))
+
+    def bvh_validate(self) -> None:
+        check(lib().rt_scene_bvh_validate(self._h))
+
     # -- measurement -------------------------------------------------------------------------
     def set_profiling(self, enabled: bool) -> None:
         check(lib().rt_set_profiling(self._h, 1 if enabled else 0))
@@ -203,6 +223,25 @@ class Scene:
 
     def reset_stats(self) -> None:
         check(lib().rt_reset_stats(self._h))
+
+    def work_stats(self, kind: int = _capi.KERNEL_CLOSEST_HIT) -> tuple[float, float]:
+        """(ray-triangle tests, BVH node visits) executed by the BVH kernels of `kind` since
+        reset_stats()."""
+        t, v = C.c_double(), C.c_double()
+        check(lib().rt_work_stats(self._h, kind, C.byref(t), C.byref(v)))
+        return t.value, v.value
+
+
+def bvh_acceptance_box(T) -> tuple[int, np.ndarray, np.ndarray]:
+    """(status, lo, hi) of the BVH's padded acceptance box for triangle T (3x3): status 0 = box,
+    1 = ill-conditioned (tested by every query), 2 = never accepted (n == 0)."""
+    t = np.ascontiguousarray(T, np.float32).reshape(9)
+    lo = np.zeros(3, np.float32)
+    hi = np.zeros(3, np.float32)
+    st = lib().rt_bvh_acceptance_box(_ptr(t), _ptr(lo), _ptr(hi))
+    if st < 0:
+        check(st)
+    return st, lo, hi
 
 
 def device_count() -> int:

@@ -1,0 +1,330 @@
+// bvh.cpp — parity-preserving BVH over the triangle records (the reference's own
+// intended acceleration, CG_Project/raytracing.cpp:167-172).
+//
+// Exactness argument. intersectMesh (raytracing.cpp:161-192) returns the lexicographic minimum of
+// (distance, index) over every triangle that rayIntersectTriangle accepts with distance < FLT_MAX.
+// That minimum does not depend on the order triangles are visited, so a traversal that (1) runs
+// the identical per-triangle test on every triangle it visits and (2) never skips a triangle that
+// could be accepted with a (distance, index) not larger than the current best returns the same
+// index and the same hit point bit for bit. (2) needs conservative boxes:
+//
+//  * Acceptance region. rayIntersectTriangle computes s, t from w = I - T0 with rounding, so an I
+//    slightly outside the triangle can be accepted. With c = |D| / (uu*vv) (sin^2 of the angle at
+//    T0) and eps = 2^-24, first-order error analysis of wu, wv (4 eps |w||u|, 4 eps |w||v|), of
+//    the products and difference in s's numerator, of uv, vv, D as rounded per-triangle values
+//    (D relative error <= 8 eps / c) and of the final division and s+t, bounds the in-plane
+//    SPATIAL displacement that any of the three tests can absorb by K eps |w| with
+//    K = 36/c + 18/c^1.5 + 2/sqrt(c). A point at distance d outside the triangle has |w| <= 2L + d
+//    (L = longest of |u|, |v|), so it can only be accepted if d <= 2 K eps L / (1 - K eps). The
+//    box is the triangle's bounding box widened by 4x that bound plus 1e-7 L.
+//  * Off-plane. I = o + r*dir with r = a/b rounded; whatever the error in r, I stays on the ray, and
+//    its distance from the plane is at most ~6 eps (|o - T0| + |I - o|). The kernel adds
+//    pad_ray = 64 eps (|o|_1 + M_1) to every box at traversal time (M_1 = max |x|+|y|+|z| of the
+//    vertices), which also covers the rounding of I itself.
+//  * Triangles with D == 0 or non-finite (then s, t are NaN/inf and the reference accepts almost
+//    anything), or with K eps > 0.05 (angle at T0 below ~1.6 degrees), are not put in the tree:
+//    every query tests them first (the "always" list). Triangles with n == 0 are rejected by
+//    isNullVector and never tested.
+//  * Box tests and the distance cull use relative slack (1e-5) far above their rounding error.
+//
+// tests/test_bvh.py checks the acceptance claim directly against the oracle's arithmetic, and
+// tests/test_gpu_parity.py checks BVH results against brute force bit for bit.
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "rt_internal.h"
+
+namespace rt {
+namespace {
+
+constexpr double kEps = 5.9604644775390625e-08;   // 2^-24
+constexpr double kMaxDelta = 0.05;   // K*eps bound for a tree triangle (pad <= 0.42 L)
+constexpr int kBins = 16;
+constexpr int kMaxLeaf = 4;
+
+struct Box {
+    float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX};
+    float hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    void grow(const Box &b) {
+        for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], b.lo[k]); hi[k] = std::max(hi[k], b.hi[k]); }
+    }
+    void grow(const float *p) {
+        for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], p[k]); hi[k] = std::max(hi[k], p[k]); }
+    }
+    bool empty() const { return lo[0] > hi[0]; }
+    double area() const {
+        if (empty()) return 0.0;
+        const double dx = double(hi[0]) - lo[0], dy = double(hi[1]) - lo[1], dz = double(hi[2]) - lo[2];
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+};
+
+struct BuildPrim {
+    Box box;
+    float centroid[3];
+    uint32_t tri;
+};
+
+struct BuildNode {
+    Box box;
+    int left = -1, right = -1;   // children (build indices) for inner nodes
+    int first = 0, count = 0;    // prim range for leaves
+};
+
+// Round a float outward by one ulp-scale step (boxes must contain the exact double bounds).
+inline float down(double v) { float f = static_cast<float>(v); return (static_cast<double>(f) > v) ? std::nextafter(f, -FLT_MAX) : f; }
+inline float up(double v) { float f = static_cast<float>(v); return (static_cast<double>(f) < v) ? std::nextafter(f, FLT_MAX) : f; }
+
+struct Builder {
+    std::vector<BuildPrim> prims;
+    std::vector<BuildNode> nodes;
+    int max_depth = 0;
+
+    int build(int first, int count, int depth) {
+        BuildNode n;
+        for (int i = 0; i < count; ++i) n.box.grow(prims[first + i].box);
+        const int id = static_cast<int>(nodes.size());
+        nodes.push_back(n);
+        max_depth = std::max(max_depth, depth);
+        if (count <= kMaxLeaf || depth >= kMaxBvhDepth - 1) {
+            nodes[id].first = first;
+            nodes[id].count = count;
+            return id;
+        }
+        Box cb;
+        for (int i = 0; i < count; ++i) cb.grow(prims[first + i].centroid);
+        int best_axis = -1, best_split = -1;
+        double best_cost = static_cast<double>(count) * n.box.area();   // cost of a leaf (intersection-only SAH)
+        for (int axis = 0; axis < 3; ++axis) {
+            const double lo = cb.lo[axis], ext = double(cb.hi[axis]) - lo;
+            if (!(ext > 0)) continue;
+            Box bb[kBins];
+            int bc[kBins] = {0};
+            for (int i = 0; i < count; ++i) {
+                int b = static_cast<int>((prims[first + i].centroid[axis] - lo) / ext * kBins);
+                b = std::min(std::max(b, 0), kBins - 1);
+                bb[b].grow(prims[first + i].box);
+                bc[b]++;
+            }
+            Box left[kBins];
+            int lc[kBins];
+            Box acc;
+            int c = 0;
+            for (int b = 0; b < kBins; ++b) { acc.grow(bb[b]); c += bc[b]; left[b] = acc; lc[b] = c; }
+            acc = Box();
+            c = 0;
+            for (int b = kBins - 1; b > 0; --b) {
+                acc.grow(bb[b]); c += bc[b];
+                const int nl = lc[b - 1];
+                if (nl == 0 || c == 0) continue;
+                const double cost = 1.0 * n.box.area() + nl * left[b - 1].area() + c * acc.area();
+                if (cost < best_cost) { best_cost = cost; best_axis = axis; best_split = b; }
+            }
+        }
+        int mid;
+        if (best_axis < 0) {
+            if (count <= 2 * kMaxLeaf) {   // no useful split: small leaf
+                nodes[id].first = first;
+                nodes[id].count = count;
+                return id;
+            }
+            // degenerate centroids: median split on the widest box axis
+            int axis = 0;
+            for (int k = 1; k < 3; ++k)
+                if (double(n.box.hi[k]) - n.box.lo[k] > double(n.box.hi[axis]) - n.box.lo[axis]) axis = k;
+            mid = first + count / 2;
+            std::nth_element(prims.begin() + first, prims.begin() + mid, prims.begin() + first + count,
+                             [axis](const BuildPrim &a, const BuildPrim &b) { return a.centroid[axis] < b.centroid[axis]; });
+        } else {
+            const double lo = cb.lo[best_axis], ext = double(cb.hi[best_axis]) - lo;
+            auto it = std::partition(prims.begin() + first, prims.begin() + first + count, [&](const BuildPrim &p) {
+                int b = static_cast<int>((p.centroid[best_axis] - lo) / ext * kBins);
+                b = std::min(std::max(b, 0), kBins - 1);
+                return b < best_split;
+            });
+            mid = static_cast<int>(it - prims.begin());
+            if (mid == first || mid == first + count) mid = first + count / 2;
+        }
+        const int l = build(first, mid - first, depth + 1);
+        const int r = build(mid, first + count - mid, depth + 1);
+        nodes[id].left = l;
+        nodes[id].right = r;
+        return id;
+    }
+};
+
+}  // namespace
+
+// Padded acceptance box of one record; returns false if the triangle must be tested by every
+// query (ill-conditioned), and sets *never if it can never be accepted (n == 0).
+bool acceptance_box(const TriRec &T, const float *v0, const float *v1, const float *v2, float lo[3], float hi[3],
+                    bool *never) {
+    *never = (T.n[0] == 0 && T.n[1] == 0 && T.n[2] == 0);
+    if (*never) return true;
+    const double uu = T.uu, vv = T.vv, D = T.D;
+    if (!std::isfinite(D) || D == 0.0 || !std::isfinite(uu) || !std::isfinite(vv) || !(uu > 0) || !(vv > 0)) return false;
+    const double c = std::fabs(D) / (uu * vv);
+    const double L = std::sqrt(std::max(uu, vv));
+    if (!std::isfinite(c) || !std::isfinite(L) || c <= 0) return false;
+    const double K = 36.0 / c + 18.0 / (c * std::sqrt(c)) + 2.0 / std::sqrt(c);
+    const double ke = K * kEps;
+    if (!(ke <= kMaxDelta)) return false;
+    const double pad = 4.0 * 2.0 * ke * L / (1.0 - ke) + 1e-7 * L;
+    for (int k = 0; k < 3; ++k) {
+        const double mn = std::min({double(v0[k]), double(v1[k]), double(v2[k])});
+        const double mx = std::max({double(v0[k]), double(v1[k]), double(v2[k])});
+        lo[k] = down(mn - pad);
+        hi[k] = up(mx + pad);
+    }
+    return true;
+}
+
+int build_bvh(const HostScene &s, const std::vector<TriRec> &recs, HostBvh &out) {
+    out = HostBvh();
+    const size_t nt = recs.size();
+    Builder b;
+    b.prims.reserve(nt);
+    double m1 = 0;
+    for (size_t i = 0; i < s.verts.size() / 3; ++i)
+        m1 = std::max(m1, std::fabs(double(s.verts[3 * i])) + std::fabs(double(s.verts[3 * i + 1])) + std::fabs(double(s.verts[3 * i + 2])));
+    out.scene_m1 = static_cast<float>(m1 * (1 + 1e-6));
+    for (size_t i = 0; i < nt; ++i) {
+        const float *v0 = &s.verts[3 * s.tris[3 * i]];
+        const float *v1 = &s.verts[3 * s.tris[3 * i + 1]];
+        const float *v2 = &s.verts[3 * s.tris[3 * i + 2]];
+        BuildPrim p;
+        bool never = false;
+        if (!acceptance_box(recs[i], v0, v1, v2, p.box.lo, p.box.hi, &never)) {
+            out.always.push_back(static_cast<uint32_t>(i));
+            continue;
+        }
+        if (never) { out.n_never++; continue; }
+        for (int k = 0; k < 3; ++k) p.centroid[k] = 0.5f * (p.box.lo[k] + p.box.hi[k]);
+        p.tri = static_cast<uint32_t>(i);
+        b.prims.push_back(p);
+    }
+    const int np = static_cast<int>(b.prims.size());
+    if (np == 0) {
+        BvhNode root{};
+        for (int k = 0; k < 3; ++k) { root.lo0[k] = root.lo1[k] = FLT_MAX; root.hi0[k] = root.hi1[k] = -FLT_MAX; }
+        root.c0 = root.c1 = kBvhEmpty;
+        out.nodes.push_back(root);
+        out.depth = 1;
+        return RT_OK;
+    }
+    b.build(0, np, 0);
+    out.depth = b.max_depth + 1;
+    // leaf order
+    out.leaf_tris.resize(np);
+    for (int i = 0; i < np; ++i) out.leaf_tris[i] = b.prims[i].tri;
+    // flatten: GPU node = an inner build node, holding both children's boxes
+    std::vector<int> gpu_id(b.nodes.size(), -1);
+    std::vector<int> order;
+    order.reserve(b.nodes.size());
+    // DFS order (left child right after parent) for locality
+    std::vector<int> st{0};
+    while (!st.empty()) {
+        const int n = st.back();
+        st.pop_back();
+        if (b.nodes[n].left < 0) continue;   // leaves are not GPU nodes
+        gpu_id[n] = static_cast<int>(order.size());
+        order.push_back(n);
+        st.push_back(b.nodes[n].right);
+        st.push_back(b.nodes[n].left);
+    }
+    auto ref_of = [&](int n) -> int32_t {
+        const BuildNode &bn = b.nodes[n];
+        if (bn.left >= 0) return gpu_id[n];
+        return static_cast<int32_t>(kBvhLeafBit | (static_cast<uint32_t>(bn.count) << kBvhCountShift) | static_cast<uint32_t>(bn.first));
+    };
+    if (np >= (1 << kBvhCountShift)) return RT_E_ARG;   // leaf first-index field overflow
+    for (const BuildNode &bn : b.nodes)
+        if (bn.left < 0 && static_cast<uint32_t>(bn.count) > kBvhCountMask) return RT_E_ARG;   // leaf too large
+    if (b.nodes[0].left < 0) {   // the whole tree is one leaf: wrap it in a root with an empty sibling
+        BvhNode root{};
+        for (int k = 0; k < 3; ++k) {
+            root.lo0[k] = b.nodes[0].box.lo[k]; root.hi0[k] = b.nodes[0].box.hi[k];
+            root.lo1[k] = FLT_MAX; root.hi1[k] = -FLT_MAX;
+        }
+        root.c0 = ref_of(0);
+        root.c1 = kBvhEmpty;
+        out.nodes.push_back(root);
+        out.depth = std::max(out.depth, 2);
+        return RT_OK;
+    }
+    out.nodes.resize(order.size());
+    for (size_t i = 0; i < order.size(); ++i) {
+        const BuildNode &bn = b.nodes[order[i]];
+        BvhNode &g = out.nodes[i];
+        const BuildNode &L = b.nodes[bn.left], &R = b.nodes[bn.right];
+        for (int k = 0; k < 3; ++k) { g.lo0[k] = L.box.lo[k]; g.hi0[k] = L.box.hi[k]; g.lo1[k] = R.box.lo[k]; g.hi1[k] = R.box.hi[k]; }
+        g.c0 = ref_of(bn.left);
+        g.c1 = ref_of(bn.right);
+    }
+    return RT_OK;
+}
+
+// Structural check used by tests: every tree triangle in exactly one leaf, every leaf's padded
+// triangle boxes inside its parent's stored child box, every node reachable, depth bound kept.
+int validate_bvh(const HostScene &s, const std::vector<TriRec> &recs, const HostBvh &h, std::string &err) {
+    const size_t nt = recs.size();
+    std::vector<int> seen(nt, 0);
+    for (uint32_t t : h.always) seen[t]++;
+    struct Item { int32_t ref; float lo[3], hi[3]; int depth; };
+    std::vector<Item> st;
+    const BvhNode &root = h.nodes[0];
+    Item a{root.c0, {root.lo0[0], root.lo0[1], root.lo0[2]}, {root.hi0[0], root.hi0[1], root.hi0[2]}, 1};
+    Item b{root.c1, {root.lo1[0], root.lo1[1], root.lo1[2]}, {root.hi1[0], root.hi1[1], root.hi1[2]}, 1};
+    st.push_back(a);
+    st.push_back(b);
+    size_t inner_seen = 1;
+    int max_stack = 0;
+    while (!st.empty()) {
+        const Item it = st.back();
+        st.pop_back();
+        if (it.ref == kBvhEmpty) continue;
+        if (it.depth > kMaxBvhDepth) { err = "depth bound exceeded"; return RT_E_PARSE; }
+        if (static_cast<uint32_t>(it.ref) & kBvhLeafBit) {
+            const uint32_t u = static_cast<uint32_t>(it.ref);
+            const uint32_t cnt = (u >> kBvhCountShift) & kBvhCountMask, first = u & ((1u << kBvhCountShift) - 1);
+            for (uint32_t i = first; i < first + cnt; ++i) {
+                const uint32_t t = h.leaf_tris[i];
+                seen[t]++;
+                float lo[3], hi[3];
+                bool never;
+                acceptance_box(recs[t], &s.verts[3 * s.tris[3 * t]], &s.verts[3 * s.tris[3 * t + 1]],
+                               &s.verts[3 * s.tris[3 * t + 2]], lo, hi, &never);
+                for (int k = 0; k < 3; ++k)
+                    if (lo[k] < it.lo[k] || hi[k] > it.hi[k]) { err = "triangle box outside its leaf box"; return RT_E_PARSE; }
+            }
+            continue;
+        }
+        const BvhNode &n = h.nodes[it.ref];
+        inner_seen++;
+        for (int k = 0; k < 3; ++k) {
+            if (n.lo0[k] < it.lo[k] || n.hi0[k] > it.hi[k] || n.lo1[k] < it.lo[k] || n.hi1[k] > it.hi[k]) {
+                err = "child box outside parent box"; return RT_E_PARSE;
+            }
+        }
+        st.push_back(Item{n.c0, {n.lo0[0], n.lo0[1], n.lo0[2]}, {n.hi0[0], n.hi0[1], n.hi0[2]}, it.depth + 1});
+        st.push_back(Item{n.c1, {n.lo1[0], n.lo1[1], n.lo1[2]}, {n.hi1[0], n.hi1[1], n.hi1[2]}, it.depth + 1});
+        max_stack = std::max(max_stack, static_cast<int>(st.size()));
+    }
+    size_t never = 0;
+    for (size_t t = 0; t < nt; ++t) {
+        const TriRec &T = recs[t];
+        const bool is_never = (T.n[0] == 0 && T.n[1] == 0 && T.n[2] == 0);
+        if (is_never) { never++; if (seen[t]) { err = "degenerate triangle in tree"; return RT_E_PARSE; } continue; }
+        if (seen[t] != 1) { err = "triangle not covered exactly once"; return RT_E_PARSE; }
+    }
+    if (inner_seen != h.nodes.size()) { err = "unreachable nodes"; return RT_E_PARSE; }
+    if (never != h.n_never) { err = "degenerate count mismatch"; return RT_E_PARSE; }
+    return RT_OK;
+}
+
+}  // namespace rt

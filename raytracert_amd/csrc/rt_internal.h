@@ -57,6 +57,36 @@ struct alignas(16) DevMaterial {
 };
 static_assert(sizeof(DevMaterial) == 64, "DevMaterial must be 64 bytes");
 
+// ---- BVH (bvh.cpp) -------------------------------------------------------------------------
+constexpr int kMaxBvhDepth = 40;                 // builder bound = GPU traversal stack depth
+constexpr uint32_t kBvhLeafBit = 0x80000000u;    // child ref: leaf | count << 21 | first
+constexpr int kBvhCountShift = 21;
+constexpr uint32_t kBvhCountMask = 0x3FFu;
+constexpr int32_t kBvhEmpty = static_cast<int32_t>(kBvhLeafBit);   // a leaf with no triangles
+
+// Two children per node, both boxes stored in the parent (64 B).
+struct alignas(16) BvhNode {
+    float lo0[3], hi0[3];
+    float lo1[3], hi1[3];
+    int32_t c0, c1;
+    int32_t pad[2];
+};
+static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 bytes");
+
+struct HostBvh {
+    std::vector<BvhNode> nodes;       // nodes[0] is the root
+    std::vector<uint32_t> leaf_tris;  // original triangle index of each leaf slot
+    std::vector<uint32_t> always;     // ill-conditioned triangles every query tests
+    size_t n_never = 0;               // n == 0: never accepted, never tested
+    int depth = 0;
+    float scene_m1 = 0;               // max |x|+|y|+|z| over vertices
+};
+
+bool acceptance_box(const TriRec &T, const float *v0, const float *v1, const float *v2, float lo[3], float hi[3],
+                    bool *never);
+int build_bvh(const HostScene &s, const std::vector<TriRec> &recs, HostBvh &out);
+int validate_bvh(const HostScene &s, const std::vector<TriRec> &recs, const HostBvh &h, std::string &err);
+
 void build_tri_records(const HostScene &s, std::vector<TriRec> &out);
 void build_dev_materials(const HostScene &s, std::vector<DevMaterial> &out);
 

@@ -44,6 +44,15 @@ struct DevScene {
     const DevMaterial *mats;
     const uint32_t *ties;           // powf(x,2) tie table
     int32_t nt, nm, n_ties, any_transparent;
+    // BVH (use_bvh != 0): nodes, leaf-ordered records and their original indices, always list
+    const BvhNode *nodes;
+    const TriRec *leaf_recs;
+    const uint32_t *leaf_idx;
+    const uint32_t *always;
+    int32_t use_bvh, n_always;
+    float scene_m1;
+    int32_t pad;
+    unsigned long long *work;       // BVH kernels' triangle tests / node visits: [0..1] closest-hit, [2..3] shadow
 };
 
 struct DevWork {

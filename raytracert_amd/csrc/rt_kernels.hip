@@ -104,8 +104,10 @@ __device__ __forceinline__ void sgpr_fence(const TriRec &T) {
                  : "memory");
 }
 
-// One rayIntersectTriangle + intersectMesh update (raytracing.cpp:106-154, :180-187).
-template <bool kAnyHit>
+// One rayIntersectTriangle + intersectMesh update (raytracing.cpp:106-154, :180-187). In index
+// order the update is the reference's strict '<' (:183); out of order (kLex, the BVH) it is the
+// equivalent lexicographic (distance, index) minimum.
+template <bool kAnyHit, bool kLex = false>
 __device__ __forceinline__ void test_triangle(const TriRec &T, int t, V3 o, V3 dir, float &best, int &bidx, V3 &bI,
                                               bool &done) {
     if (kAnyHit && done) return;
@@ -125,7 +127,7 @@ __device__ __forceinline__ void test_triangle(const TriRec &T, int t, V3 o, V3 d
     if (tt < 0 || (s + tt) > 1) return;                                         // :149
     const V3 e = sub(o, I);                                                     // distance, Vec3D.h:199-202
     const float dist = sqrtf(dot(e, e));
-    if (dist < best) {                                                          // :183
+    if (dist < best || (kLex && dist == best && t < bidx)) {                  // :183
         best = dist; bidx = t; bI = I;
         if (kAnyHit) done = true;
     }
@@ -154,6 +156,180 @@ __device__ __forceinline__ void closest_hit_loop(const TriRec *__restrict__ tris
         sgpr_fence(A);
         test_triangle<kAnyHit>(A, t, o, dir, best, bidx, bI, done);
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// BVH traversal (bvh.cpp states the exactness argument). One lane = one query; per-lane stack of
+// child refs in LDS ([depth][lane], conflict-free); nearer child first; a child is skipped when
+// its padded box misses the ray or (closest-hit) when even its entry point is farther than the
+// current best. Leaves run test_triangle on the leaf-ordered records with the original index.
+// ---------------------------------------------------------------------------------------------
+constexpr int kBvhBlock = 128;
+
+struct RayBox { V3 o, inv; float pad, dlen; };
+
+__device__ __forceinline__ bool box_hit(const RayBox &R, float lx, float ly, float lz, float hx, float hy, float hz,
+                                        float &tentry) {
+    const float ax = (lx - R.pad - R.o.x) * R.inv.x, bx = (hx + R.pad - R.o.x) * R.inv.x;
+    const float ay = (ly - R.pad - R.o.y) * R.inv.y, by = (hy + R.pad - R.o.y) * R.inv.y;
+    const float az = (lz - R.pad - R.o.z) * R.inv.z, bz = (hz + R.pad - R.o.z) * R.inv.z;
+    const float tmin = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
+    const float tmax = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    tentry = tmin;
+    return tmin <= tmax * 1.00001f;
+}
+
+template <bool kAnyHit>
+__device__ __forceinline__ void bvh_query(const DevScene &sc, V3 o, V3 dir, bool active, int &bidx, V3 &bI,
+                                          int32_t (*stack)[kBvhBlock], unsigned &tests, unsigned &visits) {
+    float best = FLT_MAX;
+    bool done = !active;
+    // ill-conditioned triangles: every query, in index order (wave-uniform scalar loads)
+    for (int i = 0; i < sc.n_always; ++i) {
+        const int t = static_cast<int>(sc.always[i]);
+        const TriRec T = sc.tris[t];
+        test_triangle<kAnyHit, true>(T, t, o, dir, best, bidx, bI, done);
+    }
+    if (!active || (kAnyHit && done)) return;
+    RayBox R;
+    R.o = o;
+    R.inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+    R.pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
+    R.dlen = sqrtf(dot(dir, dir));
+    const int lane = threadIdx.x;
+    int sp = 0;
+    int32_t ref = 0;
+    while (true) {
+        if (ref >= 0) {
+            ++visits;
+            const float4 *np = reinterpret_cast<const float4 *>(sc.nodes + ref);
+            const float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
+            float t0, t1;
+            bool h0 = box_hit(R, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, t0);
+            bool h1 = box_hit(R, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, t1);
+            if (!kAnyHit) {   // distance cull: no accepted point of the child is nearer than its entry
+                h0 = h0 && (t0 * R.dlen - R.pad) * 0.99999f <= best;
+                h1 = h1 && (t1 * R.dlen - R.pad) * 0.99999f <= best;
+            }
+            const int32_t c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
+            if (h0 && h1) {
+                const bool first0 = t0 <= t1;
+                stack[sp++][lane] = first0 ? c1 : c0;
+                ref = first0 ? c0 : c1;
+            } else if (h0) {
+                ref = c0;
+            } else if (h1) {
+                ref = c1;
+            } else {
+                if (sp == 0) break;
+                ref = stack[--sp][lane];
+            }
+        } else {
+            const uint32_t u = static_cast<uint32_t>(ref);
+            const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
+            const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
+            for (int k = 0; k < cnt; ++k) {
+                const TriRec T = sc.leaf_recs[first + k];
+                test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first + k]), o, dir, best, bidx, bI, done);
+            }
+            tests += static_cast<unsigned>(cnt);
+            if (kAnyHit && done) break;
+            if (sp == 0) break;
+            ref = stack[--sp][lane];
+        }
+    }
+}
+
+// Wave-reduce two per-lane counters and add them to the scene's work counters.
+__device__ __forceinline__ void add_work(unsigned long long *work, unsigned tests, unsigned visits) {
+    unsigned long long a = tests, b = visits;
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off);
+        b += __shfl_xor(b, off);
+    }
+    if (__lane_id() == 0 && work) {
+        atomicAdd(&work[0], a);
+        atomicAdd(&work[1], b);
+    }
+}
+
+__global__ __launch_bounds__(kBvhBlock) void k_bvh_closest_hit(const DevScene sc, const float4 *__restrict__ q_org,
+                                                               const float4 *__restrict__ q_dst,
+                                                               const int32_t *__restrict__ q_count,
+                                                               int32_t *__restrict__ hit_idx, float4 *__restrict__ hit_I) {
+    __shared__ int32_t stack[kMaxBvhDepth][kBvhBlock];
+    const int n = *q_count;
+    const int base = blockIdx.x * kBvhBlock;
+    if (base >= n) return;
+    const int j = base + threadIdx.x;
+    const bool active = j < n;
+    V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
+    if (active) {
+        const float4 qo = q_org[j], qd = q_dst[j];
+        o = mk(qo.x, qo.y, qo.z);
+        dir = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);
+    }
+    int bidx = -1;
+    V3 bI = mk(0, 0, 0);
+    unsigned tests = 0, visits = 0;
+    bvh_query<false>(sc, o, dir, active, bidx, bI, stack, tests, visits);
+    if (active) {
+        hit_idx[j] = bidx;
+        hit_I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f);
+    }
+    add_work(sc.work, tests, visits);
+}
+
+template <bool kAnyHit>
+__global__ __launch_bounds__(kBvhBlock) void k_bvh_shadow_hit(const DevScene sc, const float4 *__restrict__ q_org,
+                                                              const float4 *__restrict__ q_dst,
+                                                              const int32_t *__restrict__ q_count,
+                                                              uint8_t *__restrict__ shadow) {
+    __shared__ int32_t stack[kMaxBvhDepth][kBvhBlock];
+    const int n = *q_count;
+    const int base = blockIdx.x * kBvhBlock;
+    if (base >= n) return;
+    const int j = base + threadIdx.x;
+    const bool active = j < n;
+    V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
+    int slot = 0;
+    if (active) {
+        const float4 qo = q_org[j], qd = q_dst[j];
+        o = mk(qo.x, qo.y, qo.z);
+        dir = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);
+        slot = as_int(qo.w);
+    }
+    int bidx = -1;
+    V3 bI = mk(0, 0, 0);
+    unsigned tests = 0, visits = 0;
+    bvh_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
+    if (active) {
+        uint8_t sh = 0;
+        if (bidx >= 0) sh = sc.mats[sc.tri_mat[bidx]].transparent ? 0 : 1;
+        shadow[slot] = sh;
+    }
+    add_work(sc.work ? sc.work + 2 : nullptr, tests, visits);
+}
+
+__global__ __launch_bounds__(kBvhBlock) void k_bvh_intersect_only(const DevScene sc, const float4 *__restrict__ q_org,
+                                                                  const float4 *__restrict__ q_dst, int n,
+                                                                  int32_t *__restrict__ idx, float4 *__restrict__ I) {
+    __shared__ int32_t stack[kMaxBvhDepth][kBvhBlock];
+    const int j = blockIdx.x * kBvhBlock + threadIdx.x;
+    if (blockIdx.x * kBvhBlock >= n) return;
+    const bool active = j < n;
+    V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
+    if (active) {
+        const float4 qo = q_org[j], qd = q_dst[j];
+        o = mk(qo.x, qo.y, qo.z);
+        dir = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);
+    }
+    int bidx = -1;
+    V3 bI = mk(0, 0, 0);
+    unsigned tests = 0, visits = 0;
+    bvh_query<false>(sc, o, dir, active, bidx, bI, stack, tests, visits);
+    if (active) { idx[j] = bidx; I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f); }
+    add_work(sc.work, tests, visits);
 }
 
 __global__ __launch_bounds__(kBlock) void k_closest_hit(const TriRec *__restrict__ tris, int nt,
@@ -550,8 +726,15 @@ void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevW
     hipLaunchKernelGGL(k_gen_rays, dim3(grid_for(n)), dim3(kBlock), 0, stream, org, dst, n, w);
 }
 
+inline unsigned grid_bvh(int64_t n) { return static_cast<unsigned>((n + kBvhBlock - 1) / kBvhBlock); }
+
 void launch_closest_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
     if (capacity <= 0) return;
+    if (s.use_bvh) {
+        hipLaunchKernelGGL(k_bvh_closest_hit, dim3(grid_bvh(capacity)), dim3(kBvhBlock), 0, stream, s,
+                           w.q_org[step & 1], w.q_dst[step & 1], &w.counters[step], w.hit_idx, w.hit_I);
+        return;
+    }
     hipLaunchKernelGGL(k_closest_hit, dim3(grid_for(capacity)), dim3(kBlock), 0, stream, s.tris, s.nt,
                        w.q_org[step & 1], w.q_dst[step & 1], &w.counters[step], w.hit_idx, w.hit_I);
 }
@@ -564,6 +747,15 @@ void launch_shadow_gen(const DevScene &, const DevWork &w, const ShadeParams &p,
 
 void launch_shadow_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
     if (capacity <= 0) return;
+    if (s.use_bvh) {
+        if (s.any_transparent)
+            hipLaunchKernelGGL(k_bvh_shadow_hit<false>, dim3(grid_bvh(capacity)), dim3(kBvhBlock), 0, stream, s,
+                               w.sq_org, w.sq_dst, &w.counters[kMaxStepsCounters + step], w.shadow);
+        else
+            hipLaunchKernelGGL(k_bvh_shadow_hit<true>, dim3(grid_bvh(capacity)), dim3(kBvhBlock), 0, stream, s,
+                               w.sq_org, w.sq_dst, &w.counters[kMaxStepsCounters + step], w.shadow);
+        return;
+    }
     if (s.any_transparent)
         hipLaunchKernelGGL(k_shadow_hit<false>, dim3(grid_for(capacity)), dim3(kBlock), 0, stream, s.tris, s.nt,
                            s.tri_mat, s.mats, w.sq_org, w.sq_dst, &w.counters[kMaxStepsCounters + step], w.shadow);
@@ -591,6 +783,10 @@ void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t strea
 void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *dst, int32_t n, int32_t *idx,
                            float4 *I, hipStream_t stream) {
     if (n <= 0) return;
+    if (s.use_bvh) {
+        hipLaunchKernelGGL(k_bvh_intersect_only, dim3(grid_bvh(n)), dim3(kBvhBlock), 0, stream, s, org, dst, n, idx, I);
+        return;
+    }
     hipLaunchKernelGGL(k_intersect_only, dim3(grid_for(n)), dim3(kBlock), 0, stream, s.tris, s.nt, org, dst, n, idx, I);
 }
 

@@ -159,3 +159,81 @@ def test_transparent_shadow_path_and_deep_chain(workdir, gpu_available):
     of32, ou8, oc = O.OracleScene(path).render(O.make_params(80, 45, 2, 8, lights=lights), nthreads=16)
     assert [int(c) for c in counts] == [int(c) for c in oc]
     _assert_image_close(u8, f32, ou8, of32)
+
+
+def _query_mix(sc, rng, n):
+    """Camera rays, random rays through the scene box, secondary-like rays leaving surface points
+    (with the reference's 0.01 offset) and grazing rays."""
+    e = sc.export()
+    V, F = e["vertices"], e["triangles"]
+    lo, hi = V.min(0), V.max(0)
+    c = R.default_corners(160, 90)
+    t = rng.random((n, 2)).astype(np.float32)
+    cam_o = (c[0] * (1 - t[:, :1]) + c[6] * t[:, :1])
+    cam_d = (c[1] * (1 - t[:, 1:]) + c[7] * t[:, 1:])
+    rnd_o = lo + (hi - lo) * rng.random((n, 3)) * 1.4 - 0.2 * (hi - lo)
+    rnd_d = lo + (hi - lo) * rng.random((n, 3))
+    k = rng.integers(0, len(F), n)
+    bary = rng.random((n, 2))
+    bary[bary.sum(1) > 1] = 1 - bary[bary.sum(1) > 1]
+    P = V[F[k, 0]] + bary[:, :1] * (V[F[k, 1]] - V[F[k, 0]]) + bary[:, 1:] * (V[F[k, 2]] - V[F[k, 0]])
+    dirs = rng.normal(size=(n, 3))
+    dirs /= np.linalg.norm(dirs, axis=1)[:, None]
+    sec_o = P + 0.01 * dirs
+    sec_d = P + dirs
+    nrm = e["normals"][k]
+    gdir = dirs - (dirs * nrm).sum(1)[:, None] * nrm * (1 - 1e-3)
+    gra_o = P - gdir * 0.5
+    gra_d = P + gdir * 2.0
+    shadow_o = P + 0.1
+    shadow_d = np.tile([[0.0, 0.0, 4.0]], (n, 1))
+    o = np.concatenate([cam_o, rnd_o, sec_o, gra_o, shadow_o]).astype(np.float32)
+    d = np.concatenate([cam_d, rnd_d, sec_d, gra_d, shadow_d]).astype(np.float32)
+    return o, d
+
+
+@pytest.mark.parametrize("spec", ["ref:dodgeColorTest.obj", "ref:Models/shadow_test.obj", "syn:F4", "syn:C4"])
+def test_bvh_matches_brute_force_bitwise(spec, workdir, gpu_available):
+    path = scene_path(spec, workdir)
+    rng = np.random.default_rng(17)
+    with R.Scene.load(path, device=0) as sc:
+        o, d = _query_mix(sc, rng, 20000)
+        sc.set_accel("brute_force")
+        bi, bp = sc.intersect_mesh(o, d)
+        sc.set_accel("bvh")
+        assert sc.accel() == "bvh"
+        vi, vp = sc.intersect_mesh(o, d)
+    assert np.array_equal(bi, vi), np.nonzero(bi != vi)[0][:10]
+    assert np.array_equal(bp.view(np.uint32), vp.view(np.uint32))
+    assert (bi >= 0).sum() > 5000
+    # spot-check the brute-force answers against the oracle
+    orc = O.OracleScene(path)
+    for i in rng.choice(len(o), 150, replace=False):
+        oi, opt = orc.intersect_mesh(o[i], d[i])
+        assert oi == bi[i] and np.array_equal(opt.view(np.uint32), bp[i].view(np.uint32))
+
+
+@pytest.mark.parametrize("accel", ["brute_force", "bvh"])
+@pytest.mark.parametrize("name", ["F2b_shadow_test_160x120", "F3_spheres_128x72_pf2", "F4_refract_128x72"])
+def test_render_accel_modes_match_golden(name, accel, workdir, gpu_available):
+    entry = golden_index()[name]
+    gu8, gf32 = golden(name)
+    with R.Scene.load(scene_path(entry["scene"], workdir), device=0) as sc:
+        sc.set_accel(accel)
+        u8, f32, counts = sc.render(_params(entry), want_f32=True)
+    assert [int(c) for c in counts] == entry["counts"]
+    _assert_image_close(u8, f32, gu8, gf32)
+
+
+def test_c4_full_frame_bvh_equals_brute_force(workdir, gpu_available):
+    """The benchmark frame itself: BVH and brute-force renders of C4 1920x1080 are byte-identical
+    and issue the same queries."""
+    p = R.RenderParams(width=1920, height=1080, pf=1, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
+    with R.Scene.load(scene_path("syn:C4", workdir), device=0) as sc:
+        sc.set_accel("bvh")
+        a, af, ac = sc.render(p, want_f32=True)
+        sc.set_accel("brute_force")
+        b, bf, bc = sc.render(p, want_f32=True)
+    assert [int(x) for x in ac] == [int(x) for x in bc]
+    assert np.array_equal(a, b)
+    assert np.array_equal(af.view(np.uint32), bf.view(np.uint32))
