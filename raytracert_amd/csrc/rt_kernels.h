@@ -64,8 +64,7 @@ struct DevWork {
     float4 *chain_local;            // [step][sample]: xyz = local colour, w = child state (bits)
     float4 *chain_coef;             // [step][sample]: xyz = coefficient on the child's colour
     uint8_t *depth;                 // per sample: number of chain steps
-    int32_t *counters;              // [0..kMaxSteps] main queue counts, [kMaxSteps+1 ..] shadow counts
-    unsigned long long *rays;       // primary, secondary, shadow
+    int32_t *counters;              // [step] main queue sizes (step 0 dense, incl. inactive), [kMaxStepsCounters + step] shadow
     int64_t cap;                    // samples per batch
     int32_t steps;                  // chain steps allocated (max_lvl + 1)
 };

@@ -16,6 +16,7 @@
 // are replaced by bit-exact equivalents of glibc (threshold / tie table, see below).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <cstdint>
 
@@ -88,6 +89,35 @@ __device__ __forceinline__ int wave_append(int32_t *counter, bool pred) {
     const unsigned long long below = mask & ((1ull << lane) - 1ull);
     return pred ? base + __popcll(below) : -1;
 }
+
+// Block-wide reservation in an output queue: exclusive prefix of v over the threads of the block
+// (thread order), plus ONE atomicAdd of the block total on `counter`. A single counter word takes
+// only ~88 atomics/us (MI355X_MICROARCH.md, dequeue row), so queues are never appended per wave.
+// Every thread of the block must call it (it has barriers).
+template <int BLOCK>
+__device__ __forceinline__ int block_reserve(int v, int32_t *counter) {
+    __shared__ int s_w[BLOCK / 64 + 1];
+    const int lane = __lane_id(), wid = threadIdx.x >> 6;
+    int incl = v;
+    for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(incl, off);
+        if (lane >= off) incl += t;
+    }
+    if (lane == 63) s_w[wid] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int i = 0; i < BLOCK / 64; ++i) { const int c = s_w[i]; s_w[i] = acc; acc += c; }
+        s_w[BLOCK / 64] = acc ? atomicAdd(counter, acc) : 0;
+    }
+    __syncthreads();
+    const int r = s_w[BLOCK / 64] + s_w[wid] + incl - v;
+    __syncthreads();
+    return r;
+}
+
+constexpr int kPer = 8;           // items per thread in the chunked queue kernels
+constexpr int kMaxGrid = 2048;    // resident-size grids for grid-stride kernels (256 CUs x 8)
 
 // ---------------------------------------------------------------------------------------------
 // Closest hit: rayIntersectTriangle (raytracing.cpp:99-154) over every triangle in index order,
@@ -259,23 +289,24 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_closest_hit(const DevScene sc
                                                                int32_t *__restrict__ hit_idx, float4 *__restrict__ hit_I) {
     __shared__ int32_t stack[kMaxBvhDepth][kBvhBlock];
     const int n = *q_count;
-    const int base = blockIdx.x * kBvhBlock;
-    if (base >= n) return;
-    const int j = base + threadIdx.x;
-    const bool active = j < n;
-    V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
-    if (active) {
-        const float4 qo = q_org[j], qd = q_dst[j];
-        o = mk(qo.x, qo.y, qo.z);
-        dir = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);
-    }
-    int bidx = -1;
-    V3 bI = mk(0, 0, 0);
     unsigned tests = 0, visits = 0;
-    bvh_query<false>(sc, o, dir, active, bidx, bI, stack, tests, visits);
-    if (active) {
-        hit_idx[j] = bidx;
-        hit_I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f);
+    for (int base = blockIdx.x * kBvhBlock; base < n; base += gridDim.x * kBvhBlock) {   // resident grid-stride
+        const int j = base + threadIdx.x;
+        bool active = j < n;
+        V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
+        if (active) {
+            const float4 qo = q_org[j], qd = q_dst[j];
+            active = as_int(qd.w) >= 0;
+            o = mk(qo.x, qo.y, qo.z);
+            dir = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);
+        }
+        int bidx = -1;
+        V3 bI = mk(0, 0, 0);
+        bvh_query<false>(sc, o, dir, active, bidx, bI, stack, tests, visits);
+        if (j < n) {
+            hit_idx[j] = bidx;
+            hit_I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f);
+        }
     }
     add_work(sc.work, tests, visits);
 }
@@ -287,26 +318,26 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_shadow_hit(const DevScene sc,
                                                               uint8_t *__restrict__ shadow) {
     __shared__ int32_t stack[kMaxBvhDepth][kBvhBlock];
     const int n = *q_count;
-    const int base = blockIdx.x * kBvhBlock;
-    if (base >= n) return;
-    const int j = base + threadIdx.x;
-    const bool active = j < n;
-    V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
-    int slot = 0;
-    if (active) {
-        const float4 qo = q_org[j], qd = q_dst[j];
-        o = mk(qo.x, qo.y, qo.z);
-        dir = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);
-        slot = as_int(qo.w);
-    }
-    int bidx = -1;
-    V3 bI = mk(0, 0, 0);
     unsigned tests = 0, visits = 0;
-    bvh_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
-    if (active) {
-        uint8_t sh = 0;
-        if (bidx >= 0) sh = sc.mats[sc.tri_mat[bidx]].transparent ? 0 : 1;
-        shadow[slot] = sh;
+    for (int base = blockIdx.x * kBvhBlock; base < n; base += gridDim.x * kBvhBlock) {   // resident grid-stride
+        const int j = base + threadIdx.x;
+        const bool active = j < n;
+        V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
+        int slot = 0;
+        if (active) {
+            const float4 qo = q_org[j], qd = q_dst[j];
+            o = mk(qo.x, qo.y, qo.z);
+            dir = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);
+            slot = as_int(qo.w);
+        }
+        int bidx = -1;
+        V3 bI = mk(0, 0, 0);
+        bvh_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
+        if (active) {
+            uint8_t sh = 0;
+            if (bidx >= 0) sh = sc.mats[sc.tri_mat[bidx]].transparent ? 0 : 1;
+            shadow[slot] = sh;
+        }
     }
     add_work(sc.work ? sc.work + 2 : nullptr, tests, visits);
 }
@@ -315,20 +346,21 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_intersect_only(const DevScene
                                                                   const float4 *__restrict__ q_dst, int n,
                                                                   int32_t *__restrict__ idx, float4 *__restrict__ I) {
     __shared__ int32_t stack[kMaxBvhDepth][kBvhBlock];
-    const int j = blockIdx.x * kBvhBlock + threadIdx.x;
-    if (blockIdx.x * kBvhBlock >= n) return;
-    const bool active = j < n;
-    V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
-    if (active) {
-        const float4 qo = q_org[j], qd = q_dst[j];
-        o = mk(qo.x, qo.y, qo.z);
-        dir = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);
-    }
-    int bidx = -1;
-    V3 bI = mk(0, 0, 0);
     unsigned tests = 0, visits = 0;
-    bvh_query<false>(sc, o, dir, active, bidx, bI, stack, tests, visits);
-    if (active) { idx[j] = bidx; I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f); }
+    for (int base = blockIdx.x * kBvhBlock; base < n; base += gridDim.x * kBvhBlock) {
+        const int j = base + threadIdx.x;
+        const bool active = j < n;
+        V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
+        if (active) {
+            const float4 qo = q_org[j], qd = q_dst[j];
+            o = mk(qo.x, qo.y, qo.z);
+            dir = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);
+        }
+        int bidx = -1;
+        V3 bI = mk(0, 0, 0);
+        bvh_query<false>(sc, o, dir, active, bidx, bI, stack, tests, visits);
+        if (active) { idx[j] = bidx; I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f); }
+    }
     add_work(sc.work, tests, visits);
 }
 
@@ -341,17 +373,18 @@ __global__ __launch_bounds__(kBlock) void k_closest_hit(const TriRec *__restrict
     const int base = blockIdx.x * kBlock;
     if (base >= n) return;
     const int j = base + threadIdx.x;
-    const bool active = j < n;
+    bool active = j < n;
     V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
     if (active) {
         const float4 qo = q_org[j], qd = q_dst[j];
+        active = as_int(qd.w) >= 0;                                                 // lvl -1: outside the frame
         o = mk(qo.x, qo.y, qo.z);
         dir = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);                          // :111
     }
     int bidx = -1;
     V3 bI = mk(0, 0, 0);
     closest_hit_loop<false>(tris, nt, o, dir, active, bidx, bI);
-    if (active) {
+    if (j < n) {
         hit_idx[j] = bidx;
         hit_I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f);
     }
@@ -424,59 +457,51 @@ __device__ __forceinline__ bool decode_pixel(const FrameGeom &g, int64_t pix, in
     return x < g.width && y < g.height && x < g.ox + g.cw && y < g.oy + g.ch && x >= 0 && y >= 0;
 }
 
+// The primary queue is dense: query s is sample s, so no compaction (and no atomics) at all;
+// samples outside the frame or the clip rectangle are marked inactive with lvl = -1.
 __global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWork w) {
     const int spp = g.pfx * g.pfy;
     const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th * spp;
     const int64_t s = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    bool valid = false;
+    if (s >= n) return;
+    if (s == 0) w.counters[0] = static_cast<int32_t>(n);
+    const int64_t pix = s / spp;
+    const int sub = static_cast<int>(s - pix * spp);
+    const int subx = sub / g.pfy, suby = sub - subx * g.pfy;   // subx outer, suby inner (:377-378)
+    int x, y;
+    const bool valid = decode_pixel(g, pix, x, y);
     V3 origin = mk(0, 0, 0), dest = mk(0, 0, 0);
-    if (s < n) {
-        const int64_t pix = s / spp;
-        const int sub = static_cast<int>(s - pix * spp);
-        const int subx = sub / g.pfy, suby = sub - subx * g.pfy;   // subx outer, suby inner (:377-378)
-        int x, y;
-        valid = decode_pixel(g, pix, x, y);
-        if (valid) {
-            const float xscale = 1.0f - (static_cast<float>(static_cast<unsigned>(x)) * static_cast<float>(static_cast<unsigned>(g.pfx)) + static_cast<float>(subx)) / g.divX;  // :380
-            const float yscale = 1.0f - (static_cast<float>(static_cast<unsigned>(y)) * static_cast<float>(static_cast<unsigned>(g.pfy)) + static_cast<float>(suby)) / g.divY;  // :381
-            const V3 o00 = mk(g.corners[0][0], g.corners[0][1], g.corners[0][2]);
-            const V3 d00 = mk(g.corners[1][0], g.corners[1][1], g.corners[1][2]);
-            const V3 o01 = mk(g.corners[2][0], g.corners[2][1], g.corners[2][2]);
-            const V3 d01 = mk(g.corners[3][0], g.corners[3][1], g.corners[3][2]);
-            const V3 o10 = mk(g.corners[4][0], g.corners[4][1], g.corners[4][2]);
-            const V3 d10 = mk(g.corners[5][0], g.corners[5][1], g.corners[5][2]);
-            const V3 o11 = mk(g.corners[6][0], g.corners[6][1], g.corners[6][2]);
-            const V3 d11 = mk(g.corners[7][0], g.corners[7][1], g.corners[7][2]);
-            const float ix = 1 - xscale, iy = 1 - yscale;
-            origin = add(scale(add(scale(o00, xscale), scale(o10, ix)), yscale),
-                         scale(add(scale(o01, xscale), scale(o11, ix)), iy));                     // :383-384
-            dest = add(scale(add(scale(d00, xscale), scale(d10, ix)), yscale),
-                       scale(add(scale(d01, xscale), scale(d11, ix)), iy));                       // :385-386
-        }
-        if (s < w.cap) w.depth[s] = 0;
-    }
-    const int pos = wave_append(&w.counters[0], valid);
     if (valid) {
-        w.q_org[0][pos] = make_float4(origin.x, origin.y, origin.z, as_float(static_cast<int>(s)));
-        w.q_dst[0][pos] = make_float4(dest.x, dest.y, dest.z, as_float(0));
+        const float xscale = 1.0f - (static_cast<float>(static_cast<unsigned>(x)) * static_cast<float>(static_cast<unsigned>(g.pfx)) + static_cast<float>(subx)) / g.divX;  // :380
+        const float yscale = 1.0f - (static_cast<float>(static_cast<unsigned>(y)) * static_cast<float>(static_cast<unsigned>(g.pfy)) + static_cast<float>(suby)) / g.divY;  // :381
+        const V3 o00 = mk(g.corners[0][0], g.corners[0][1], g.corners[0][2]);
+        const V3 d00 = mk(g.corners[1][0], g.corners[1][1], g.corners[1][2]);
+        const V3 o01 = mk(g.corners[2][0], g.corners[2][1], g.corners[2][2]);
+        const V3 d01 = mk(g.corners[3][0], g.corners[3][1], g.corners[3][2]);
+        const V3 o10 = mk(g.corners[4][0], g.corners[4][1], g.corners[4][2]);
+        const V3 d10 = mk(g.corners[5][0], g.corners[5][1], g.corners[5][2]);
+        const V3 o11 = mk(g.corners[6][0], g.corners[6][1], g.corners[6][2]);
+        const V3 d11 = mk(g.corners[7][0], g.corners[7][1], g.corners[7][2]);
+        const float ix = 1 - xscale, iy = 1 - yscale;
+        origin = add(scale(add(scale(o00, xscale), scale(o10, ix)), yscale),
+                     scale(add(scale(o01, xscale), scale(o11, ix)), iy));                     // :383-384
+        dest = add(scale(add(scale(d00, xscale), scale(d10, ix)), yscale),
+                   scale(add(scale(d01, xscale), scale(d11, ix)), iy));                       // :385-386
     }
-    const unsigned long long m = __ballot(valid);
-    if (__lane_id() == 0 && m) atomicAdd(&w.rays[0], static_cast<unsigned long long>(__popcll(m)));
+    w.depth[s] = 0;
+    w.q_org[0][s] = make_float4(origin.x, origin.y, origin.z, as_float(static_cast<int>(s)));
+    w.q_dst[0][s] = make_float4(dest.x, dest.y, dest.z, as_float(valid ? 0 : -1));
 }
 
 __global__ __launch_bounds__(kBlock) void k_gen_rays(const float4 *__restrict__ org, const float4 *__restrict__ dst,
                                                      int32_t n, DevWork w) {
     const int s = blockIdx.x * kBlock + threadIdx.x;
-    const bool valid = s < n;
-    const int pos = wave_append(&w.counters[0], valid);
-    if (valid) {
-        const float4 o = org[s], d = dst[s];
-        w.q_org[0][pos] = make_float4(o.x, o.y, o.z, as_float(s));
-        w.q_dst[0][pos] = make_float4(d.x, d.y, d.z, as_float(0));
-        w.depth[s] = 0;
-    }
-    const unsigned long long m = __ballot(valid);
-    if (__lane_id() == 0 && m) atomicAdd(&w.rays[0], static_cast<unsigned long long>(__popcll(m)));
+    if (s >= n) return;
+    if (s == 0) w.counters[0] = n;
+    const float4 o = org[s], d = dst[s];
+    w.q_org[0][s] = make_float4(o.x, o.y, o.z, as_float(s));
+    w.q_dst[0][s] = make_float4(d.x, d.y, d.z, as_float(0));
+    w.depth[s] = 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -484,25 +509,52 @@ __global__ __launch_bounds__(kBlock) void k_gen_rays(const float4 *__restrict__ 
 // (raytracing.cpp:246), destination = light position (:248).
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_shadow_gen(const ShadeParams p, DevWork w) {
-    const int slot_q = blockIdx.x * kBlock + threadIdx.x;          // (query, light) pair
     const int L = p.n_lights;
-    const int n = w.counters[p.step];
-    const int j = slot_q / L, l = slot_q - j * L;
-    bool valid = false;
-    float4 so = make_float4(0, 0, 0, 0), sd = so;
-    if (j < n) {
-        if (w.hit_idx[j] >= 0) {
+    const int total = w.counters[p.step] * L;                  // (query, light) pairs
+    for (int base = blockIdx.x * kBlock * kPer; base < total; base += gridDim.x * kBlock * kPer) {
+        const int first = base + threadIdx.x * kPer;
+        int cnt = 0;
+        for (int k = 0; k < kPer; ++k) {
+            const int slot = first + k;
+            if (slot < total && w.hit_idx[slot / L] >= 0) ++cnt;
+        }
+        int pos = block_reserve<kBlock>(cnt, &w.counters[kMaxStepsCounters + p.step]);
+        for (int k = 0; k < kPer; ++k) {
+            const int slot = first + k;
+            if (slot >= total) break;
+            const int j = slot / L, l = slot - j * L;
+            if (w.hit_idx[j] < 0) continue;
             const float4 I = w.hit_I[j];
-            so = make_float4(I.x + 0.1f, I.y + 0.1f, I.z + 0.1f, as_float(slot_q));
-            sd = make_float4(p.lights[l][0], p.lights[l][1], p.lights[l][2], 0.0f);
-            valid = true;
+            w.sq_org[pos] = make_float4(I.x + 0.1f, I.y + 0.1f, I.z + 0.1f, as_float(slot));
+            w.sq_dst[pos] = make_float4(p.lights[l][0], p.lights[l][1], p.lights[l][2], 0.0f);
+            ++pos;
         }
     }
-    if (blockIdx.x * kBlock >= n * L) return;   // whole block past the end: uniform exit
-    const int pos = wave_append(&w.counters[kMaxStepsCounters + p.step], valid);
-    if (valid) { w.sq_org[pos] = so; w.sq_dst[pos] = sd; }
-    const unsigned long long m = __ballot(valid);
-    if (__lane_id() == 0 && m) atomicAdd(&w.rays[2], static_cast<unsigned long long>(__popcll(m)));
+}
+
+// Compacts the secondary rays k_shade left densely in sq_org/sq_dst (lvl < 0 = none) into the
+// next step's queue, in order, one atomic per block chunk.
+__global__ __launch_bounds__(kBlock) void k_compact_next(const ShadeParams p, DevWork w) {
+    const int total = w.counters[p.step];
+    const int nb = (p.step + 1) & 1;
+    for (int base = blockIdx.x * kBlock * kPer; base < total; base += gridDim.x * kBlock * kPer) {
+        const int first = base + threadIdx.x * kPer;
+        int cnt = 0;
+        for (int k = 0; k < kPer; ++k) {
+            const int j = first + k;
+            if (j < total && as_int(w.sq_dst[j].w) >= 0) ++cnt;
+        }
+        int pos = block_reserve<kBlock>(cnt, &w.counters[p.step + 1]);
+        for (int k = 0; k < kPer; ++k) {
+            const int j = first + k;
+            if (j >= total) break;
+            const float4 d = w.sq_dst[j];
+            if (as_int(d.w) < 0) continue;
+            w.q_org[nb][pos] = w.sq_org[j];
+            w.q_dst[nb][pos] = d;
+            ++pos;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -534,18 +586,22 @@ __device__ __forceinline__ void offset_point(V3 &point, V3 dest) {   // addOffse
     point = add(point, v);
 }
 
+// One lane per query, grid-stride over the step's queue. The secondary ray (if any) is written
+// densely at the query's position in sq_org/sq_dst (lvl -1 = none; the shadow queue is consumed
+// by then) and compacted into the next queue by k_compact_next.
 __global__ __launch_bounds__(kBlock) void k_shade(const DevScene sc, const ShadeParams p, DevWork w) {
-    const int j = blockIdx.x * kBlock + threadIdx.x;
     const int n = w.counters[p.step];
-    if (blockIdx.x * kBlock >= n) return;
-    const bool active = j < n;
+    for (int j = blockIdx.x * kBlock + threadIdx.x; j < n; j += gridDim.x * kBlock) {
     Secondary sec;
     sec.state = kChildNone;
+    sec.org = mk(0, 0, 0);
+    sec.dst = mk(0, 0, 0);
+    sec.lvl = -1;
     int sample = 0;
-    if (active) {
-        const float4 qo = w.q_org[p.step & 1][j], qd = w.q_dst[p.step & 1][j];
+    const float4 qo = w.q_org[p.step & 1][j], qd = w.q_dst[p.step & 1][j];
+    const int lvl = as_int(qd.w);
+    if (lvl >= 0) {                                                       // inactive (outside frame) otherwise
         sample = as_int(qo.w);
-        const int lvl = as_int(qd.w);
         const int idx = w.hit_idx[j];
         const int64_t ci = static_cast<int64_t>(p.step) * w.cap + sample;
         if (idx < 0) {                                                   // trace() miss -> BLACK (:389-391)
@@ -638,15 +694,10 @@ __global__ __launch_bounds__(kBlock) void k_shade(const DevScene sc, const Shade
             else w.depth[sample] = static_cast<uint8_t>(p.step + 1);
         }
     }
-    const bool spawn = active && sec.state == kChildTrace;
-    const int pos = wave_append(&w.counters[p.step + 1], spawn);
-    if (spawn) {
-        const int nb = (p.step + 1) & 1;
-        w.q_org[nb][pos] = make_float4(sec.org.x, sec.org.y, sec.org.z, as_float(sample));
-        w.q_dst[nb][pos] = make_float4(sec.dst.x, sec.dst.y, sec.dst.z, as_float(sec.lvl));
+    const bool spawn = sec.state == kChildTrace;
+    w.sq_org[j] = make_float4(sec.org.x, sec.org.y, sec.org.z, as_float(sample));
+    w.sq_dst[j] = make_float4(sec.dst.x, sec.dst.y, sec.dst.z, as_float(spawn ? sec.lvl : -1));
     }
-    const unsigned long long m2 = __ballot(spawn);
-    if (__lane_id() == 0 && m2) atomicAdd(&w.rays[1], static_cast<unsigned long long>(__popcll(m2)));
 }
 
 // Fold one sample's chain back to front: c_k = local_k + coef_k * c_{k+1} (the order in which
@@ -726,7 +777,15 @@ void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevW
     hipLaunchKernelGGL(k_gen_rays, dim3(grid_for(n)), dim3(kBlock), 0, stream, org, dst, n, w);
 }
 
-inline unsigned grid_bvh(int64_t n) { return static_cast<unsigned>((n + kBvhBlock - 1) / kBvhBlock); }
+inline unsigned grid_bvh(int64_t n) {
+    return static_cast<unsigned>(std::min<int64_t>((n + kBvhBlock - 1) / kBvhBlock, kMaxGrid));
+}
+inline unsigned grid_chunked(int64_t n) {
+    return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n + kBlock * kPer - 1) / (kBlock * kPer), kMaxGrid)));
+}
+inline unsigned grid_stride(int64_t n) {
+    return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, kMaxGrid)));
+}
 
 void launch_closest_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
     if (capacity <= 0) return;
@@ -742,7 +801,7 @@ void launch_closest_hit(const DevScene &s, const DevWork &w, int step, int64_t c
 void launch_shadow_gen(const DevScene &, const DevWork &w, const ShadeParams &p, int64_t capacity, hipStream_t stream) {
     const int64_t n = capacity * p.n_lights;
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_shadow_gen, dim3(grid_for(n)), dim3(kBlock), 0, stream, p, w);
+    hipLaunchKernelGGL(k_shadow_gen, dim3(grid_chunked(n)), dim3(kBlock), 0, stream, p, w);
 }
 
 void launch_shadow_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
@@ -766,7 +825,8 @@ void launch_shadow_hit(const DevScene &s, const DevWork &w, int step, int64_t ca
 
 void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int64_t capacity, hipStream_t stream) {
     if (capacity <= 0) return;
-    hipLaunchKernelGGL(k_shade, dim3(grid_for(capacity)), dim3(kBlock), 0, stream, s, p, w);
+    hipLaunchKernelGGL(k_shade, dim3(grid_stride(capacity)), dim3(kBlock), 0, stream, s, p, w);
+    hipLaunchKernelGGL(k_compact_next, dim3(grid_chunked(capacity)), dim3(kBlock), 0, stream, p, w);
 }
 
 void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream) {
