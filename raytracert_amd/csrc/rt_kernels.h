@@ -51,7 +51,7 @@ struct DevScene {
     const uint32_t *always;
     int32_t use_bvh, n_always;
     float scene_m1;
-    int32_t pad;
+    int32_t bvh_depth;              // traversal stack entries needed (tree depth)
     unsigned long long *work;       // BVH kernels' triangle tests / node visits: [0..1] closest-hit, [2..3] shadow
 };
 

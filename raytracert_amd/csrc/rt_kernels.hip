@@ -90,30 +90,35 @@ __device__ __forceinline__ int wave_append(int32_t *counter, bool pred) {
     return pred ? base + __popcll(below) : -1;
 }
 
-// Block-wide reservation in an output queue: exclusive prefix of v over the threads of the block
-// (thread order), plus ONE atomicAdd of the block total on `counter`. A single counter word takes
-// only ~88 atomics/us (MI355X_MICROARCH.md, dequeue row), so queues are never appended per wave.
-// Every thread of the block must call it (it has barriers).
-template <int BLOCK>
-__device__ __forceinline__ int block_reserve(int v, int32_t *counter) {
-    __shared__ int s_w[BLOCK / 64 + 1];
+// Block-wide reservation in an output queue for kPer coalesced rounds of items: round k covers
+// items base + k*BLOCK + threadIdx.x, so reads and writes stay coalesced and the output keeps
+// input order. One atomicAdd per block chunk: a single counter word takes only ~88 atomics/us
+// (MI355X_MICROARCH.md, dequeue row), so queues are never appended per wave. Returns, for each
+// round, this thread's output slot (or -1). Every thread of the block must call it (barriers).
+template <int BLOCK, int PER>
+__device__ __forceinline__ void block_reserve_rounds(const bool (&valid)[PER], int32_t *counter, int (&pos)[PER]) {
+    constexpr int NW = BLOCK / 64;
+    __shared__ int s_c[PER * NW + 1];
     const int lane = __lane_id(), wid = threadIdx.x >> 6;
-    int incl = v;
-    for (int off = 1; off < 64; off <<= 1) {
-        const int t = __shfl_up(incl, off);
-        if (lane >= off) incl += t;
+    unsigned long long m[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        m[k] = __ballot(valid[k]);
+        if (lane == 0) s_c[k * NW + wid] = __popcll(m[k]);
     }
-    if (lane == 63) s_w[wid] = incl;
     __syncthreads();
     if (threadIdx.x == 0) {
         int acc = 0;
-        for (int i = 0; i < BLOCK / 64; ++i) { const int c = s_w[i]; s_w[i] = acc; acc += c; }
-        s_w[BLOCK / 64] = acc ? atomicAdd(counter, acc) : 0;
+        for (int i = 0; i < PER * NW; ++i) { const int c = s_c[i]; s_c[i] = acc; acc += c; }
+        s_c[PER * NW] = acc ? atomicAdd(counter, acc) : 0;
     }
     __syncthreads();
-    const int r = s_w[BLOCK / 64] + s_w[wid] + incl - v;
+    const int base = s_c[PER * NW];
+    const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+        pos[k] = valid[k] ? base + s_c[k * NW + wid] + __popcll(m[k] & below) : -1;
     __syncthreads();
-    return r;
 }
 
 constexpr int kPer = 8;           // items per thread in the chunked queue kernels
@@ -287,7 +292,8 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_closest_hit(const DevScene sc
                                                                const float4 *__restrict__ q_dst,
                                                                const int32_t *__restrict__ q_count,
                                                                int32_t *__restrict__ hit_idx, float4 *__restrict__ hit_I) {
-    __shared__ int32_t stack[kMaxBvhDepth][kBvhBlock];
+    extern __shared__ int32_t lds_stack[];
+    int32_t (*stack)[kBvhBlock] = reinterpret_cast<int32_t (*)[kBvhBlock]>(lds_stack);
     const int n = *q_count;
     unsigned tests = 0, visits = 0;
     for (int base = blockIdx.x * kBvhBlock; base < n; base += gridDim.x * kBvhBlock) {   // resident grid-stride
@@ -316,7 +322,8 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_shadow_hit(const DevScene sc,
                                                               const float4 *__restrict__ q_dst,
                                                               const int32_t *__restrict__ q_count,
                                                               uint8_t *__restrict__ shadow) {
-    __shared__ int32_t stack[kMaxBvhDepth][kBvhBlock];
+    extern __shared__ int32_t lds_stack[];
+    int32_t (*stack)[kBvhBlock] = reinterpret_cast<int32_t (*)[kBvhBlock]>(lds_stack);
     const int n = *q_count;
     unsigned tests = 0, visits = 0;
     for (int base = blockIdx.x * kBvhBlock; base < n; base += gridDim.x * kBvhBlock) {   // resident grid-stride
@@ -345,7 +352,8 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_shadow_hit(const DevScene sc,
 __global__ __launch_bounds__(kBvhBlock) void k_bvh_intersect_only(const DevScene sc, const float4 *__restrict__ q_org,
                                                                   const float4 *__restrict__ q_dst, int n,
                                                                   int32_t *__restrict__ idx, float4 *__restrict__ I) {
-    __shared__ int32_t stack[kMaxBvhDepth][kBvhBlock];
+    extern __shared__ int32_t lds_stack[];
+    int32_t (*stack)[kBvhBlock] = reinterpret_cast<int32_t (*)[kBvhBlock]>(lds_stack);
     unsigned tests = 0, visits = 0;
     for (int base = blockIdx.x * kBvhBlock; base < n; base += gridDim.x * kBvhBlock) {
         const int j = base + threadIdx.x;
@@ -512,47 +520,48 @@ __global__ __launch_bounds__(kBlock) void k_shadow_gen(const ShadeParams p, DevW
     const int L = p.n_lights;
     const int total = w.counters[p.step] * L;                  // (query, light) pairs
     for (int base = blockIdx.x * kBlock * kPer; base < total; base += gridDim.x * kBlock * kPer) {
-        const int first = base + threadIdx.x * kPer;
-        int cnt = 0;
+        bool valid[kPer];
+        int pos[kPer];
+#pragma unroll
         for (int k = 0; k < kPer; ++k) {
-            const int slot = first + k;
-            if (slot < total && w.hit_idx[slot / L] >= 0) ++cnt;
+            const int slot = base + k * kBlock + threadIdx.x;
+            valid[k] = slot < total && w.hit_idx[slot / L] >= 0;
         }
-        int pos = block_reserve<kBlock>(cnt, &w.counters[kMaxStepsCounters + p.step]);
+        block_reserve_rounds<kBlock, kPer>(valid, &w.counters[kMaxStepsCounters + p.step], pos);
+#pragma unroll
         for (int k = 0; k < kPer; ++k) {
-            const int slot = first + k;
-            if (slot >= total) break;
+            if (!valid[k]) continue;
+            const int slot = base + k * kBlock + threadIdx.x;
             const int j = slot / L, l = slot - j * L;
-            if (w.hit_idx[j] < 0) continue;
             const float4 I = w.hit_I[j];
-            w.sq_org[pos] = make_float4(I.x + 0.1f, I.y + 0.1f, I.z + 0.1f, as_float(slot));
-            w.sq_dst[pos] = make_float4(p.lights[l][0], p.lights[l][1], p.lights[l][2], 0.0f);
-            ++pos;
+            w.sq_org[pos[k]] = make_float4(I.x + 0.1f, I.y + 0.1f, I.z + 0.1f, as_float(slot));
+            w.sq_dst[pos[k]] = make_float4(p.lights[l][0], p.lights[l][1], p.lights[l][2], 0.0f);
         }
     }
 }
 
 // Compacts the secondary rays k_shade left densely in sq_org/sq_dst (lvl < 0 = none) into the
-// next step's queue, in order, one atomic per block chunk.
+// next step's queue, in order.
 __global__ __launch_bounds__(kBlock) void k_compact_next(const ShadeParams p, DevWork w) {
     const int total = w.counters[p.step];
     const int nb = (p.step + 1) & 1;
     for (int base = blockIdx.x * kBlock * kPer; base < total; base += gridDim.x * kBlock * kPer) {
-        const int first = base + threadIdx.x * kPer;
-        int cnt = 0;
+        bool valid[kPer];
+        int pos[kPer];
+        float4 d[kPer];
+#pragma unroll
         for (int k = 0; k < kPer; ++k) {
-            const int j = first + k;
-            if (j < total && as_int(w.sq_dst[j].w) >= 0) ++cnt;
+            const int j = base + k * kBlock + threadIdx.x;
+            d[k] = j < total ? w.sq_dst[j] : make_float4(0, 0, 0, as_float(-1));
+            valid[k] = as_int(d[k].w) >= 0;
         }
-        int pos = block_reserve<kBlock>(cnt, &w.counters[p.step + 1]);
+        block_reserve_rounds<kBlock, kPer>(valid, &w.counters[p.step + 1], pos);
+#pragma unroll
         for (int k = 0; k < kPer; ++k) {
-            const int j = first + k;
-            if (j >= total) break;
-            const float4 d = w.sq_dst[j];
-            if (as_int(d.w) < 0) continue;
-            w.q_org[nb][pos] = w.sq_org[j];
-            w.q_dst[nb][pos] = d;
-            ++pos;
+            if (!valid[k]) continue;
+            const int j = base + k * kBlock + threadIdx.x;
+            w.q_org[nb][pos[k]] = w.sq_org[j];
+            w.q_dst[nb][pos[k]] = d[k];
         }
     }
 }
@@ -777,6 +786,9 @@ void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevW
     hipLaunchKernelGGL(k_gen_rays, dim3(grid_for(n)), dim3(kBlock), 0, stream, org, dst, n, w);
 }
 
+// LDS stack bytes: one int per tree level per lane (the builder bounds the depth by kMaxBvhDepth)
+inline size_t bvh_lds(const DevScene &s) { return sizeof(int32_t) * kBvhBlock * static_cast<size_t>(s.bvh_depth); }
+
 inline unsigned grid_bvh(int64_t n) {
     return static_cast<unsigned>(std::min<int64_t>((n + kBvhBlock - 1) / kBvhBlock, kMaxGrid));
 }
@@ -790,7 +802,7 @@ inline unsigned grid_stride(int64_t n) {
 void launch_closest_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
     if (capacity <= 0) return;
     if (s.use_bvh) {
-        hipLaunchKernelGGL(k_bvh_closest_hit, dim3(grid_bvh(capacity)), dim3(kBvhBlock), 0, stream, s,
+        hipLaunchKernelGGL(k_bvh_closest_hit, dim3(grid_bvh(capacity)), dim3(kBvhBlock), bvh_lds(s), stream, s,
                            w.q_org[step & 1], w.q_dst[step & 1], &w.counters[step], w.hit_idx, w.hit_I);
         return;
     }
@@ -808,10 +820,10 @@ void launch_shadow_hit(const DevScene &s, const DevWork &w, int step, int64_t ca
     if (capacity <= 0) return;
     if (s.use_bvh) {
         if (s.any_transparent)
-            hipLaunchKernelGGL(k_bvh_shadow_hit<false>, dim3(grid_bvh(capacity)), dim3(kBvhBlock), 0, stream, s,
+            hipLaunchKernelGGL(k_bvh_shadow_hit<false>, dim3(grid_bvh(capacity)), dim3(kBvhBlock), bvh_lds(s), stream, s,
                                w.sq_org, w.sq_dst, &w.counters[kMaxStepsCounters + step], w.shadow);
         else
-            hipLaunchKernelGGL(k_bvh_shadow_hit<true>, dim3(grid_bvh(capacity)), dim3(kBvhBlock), 0, stream, s,
+            hipLaunchKernelGGL(k_bvh_shadow_hit<true>, dim3(grid_bvh(capacity)), dim3(kBvhBlock), bvh_lds(s), stream, s,
                                w.sq_org, w.sq_dst, &w.counters[kMaxStepsCounters + step], w.shadow);
         return;
     }
@@ -844,7 +856,7 @@ void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *d
                            float4 *I, hipStream_t stream) {
     if (n <= 0) return;
     if (s.use_bvh) {
-        hipLaunchKernelGGL(k_bvh_intersect_only, dim3(grid_bvh(n)), dim3(kBvhBlock), 0, stream, s, org, dst, n, idx, I);
+        hipLaunchKernelGGL(k_bvh_intersect_only, dim3(grid_bvh(n)), dim3(kBvhBlock), bvh_lds(s), stream, s, org, dst, n, idx, I);
         return;
     }
     hipLaunchKernelGGL(k_intersect_only, dim3(grid_for(n)), dim3(kBlock), 0, stream, s.tris, s.nt, org, dst, n, idx, I);
