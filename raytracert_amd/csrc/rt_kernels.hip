@@ -275,6 +275,25 @@ __device__ __forceinline__ void bvh_query(const DevScene &sc, V3 o, V3 dir, bool
     }
 }
 
+// XCD-aware work split (cdna_hip_programming.md T1): blocks are dealt round-robin over the 8 XCDs,
+// so blocks b and b+8 share an XCD's L2. Queues are in screen order (tiles row-major, children
+// after their parents), so giving each XCD one contiguous eighth of the queue keeps the part of
+// the scene it touches small enough to stay in its 4 MB L2. Placement only changes speed.
+constexpr int kXcds = 8;
+struct Segment { int begin, end, step, start; };
+__device__ __forceinline__ Segment xcd_segment(int n, int block_dim) {
+    const int xcd = blockIdx.x % kXcds;
+    const int per_xcd_blocks = (gridDim.x + kXcds - 1 - xcd) / kXcds;    // blocks with this residue
+    const int local = blockIdx.x / kXcds;
+    const int chunk = (n + kXcds - 1) / kXcds;
+    Segment g;
+    g.begin = min(n, xcd * chunk);
+    g.end = min(n, g.begin + chunk);
+    g.step = per_xcd_blocks * block_dim;
+    g.start = g.begin + local * block_dim;
+    return g;
+}
+
 // Wave-reduce two per-lane counters and add them to the scene's work counters.
 __device__ __forceinline__ void add_work(unsigned long long *work, unsigned tests, unsigned visits) {
     unsigned long long a = tests, b = visits;
@@ -296,9 +315,10 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_closest_hit(const DevScene sc
     int32_t (*stack)[kBvhBlock] = reinterpret_cast<int32_t (*)[kBvhBlock]>(lds_stack);
     const int n = *q_count;
     unsigned tests = 0, visits = 0;
-    for (int base = blockIdx.x * kBvhBlock; base < n; base += gridDim.x * kBvhBlock) {   // resident grid-stride
+    const Segment seg = xcd_segment(n, kBvhBlock);
+    for (int base = seg.start; base < seg.end; base += seg.step) {   // resident grid-stride within the XCD's segment
         const int j = base + threadIdx.x;
-        bool active = j < n;
+        bool active = j < seg.end;
         V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
         if (active) {
             const float4 qo = q_org[j], qd = q_dst[j];
@@ -309,7 +329,7 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_closest_hit(const DevScene sc
         int bidx = -1;
         V3 bI = mk(0, 0, 0);
         bvh_query<false>(sc, o, dir, active, bidx, bI, stack, tests, visits);
-        if (j < n) {
+        if (j < seg.end) {
             hit_idx[j] = bidx;
             hit_I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f);
         }
@@ -326,9 +346,10 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_shadow_hit(const DevScene sc,
     int32_t (*stack)[kBvhBlock] = reinterpret_cast<int32_t (*)[kBvhBlock]>(lds_stack);
     const int n = *q_count;
     unsigned tests = 0, visits = 0;
-    for (int base = blockIdx.x * kBvhBlock; base < n; base += gridDim.x * kBvhBlock) {   // resident grid-stride
+    const Segment seg = xcd_segment(n, kBvhBlock);
+    for (int base = seg.start; base < seg.end; base += seg.step) {   // resident grid-stride within the XCD's segment
         const int j = base + threadIdx.x;
-        const bool active = j < n;
+        const bool active = j < seg.end;
         V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
         int slot = 0;
         if (active) {
@@ -789,8 +810,10 @@ void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevW
 // LDS stack bytes: one int per tree level per lane (the builder bounds the depth by kMaxBvhDepth)
 inline size_t bvh_lds(const DevScene &s) { return sizeof(int32_t) * kBvhBlock * static_cast<size_t>(s.bvh_depth); }
 
+// 128-thread blocks with a 10-20 KB LDS stack: 16 resident per CU (32 waves) -> 4096 blocks.
+constexpr int kMaxBvhGrid = 4096;
 inline unsigned grid_bvh(int64_t n) {
-    return static_cast<unsigned>(std::min<int64_t>((n + kBvhBlock - 1) / kBvhBlock, kMaxGrid));
+    return static_cast<unsigned>(std::min<int64_t>((n + kBvhBlock - 1) / kBvhBlock, kMaxBvhGrid));
 }
 inline unsigned grid_chunked(int64_t n) {
     return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n + kBlock * kPer - 1) / (kBlock * kPer), kMaxGrid)));
