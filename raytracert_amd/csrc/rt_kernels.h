@@ -70,6 +70,7 @@ struct DevWork {
 };
 
 constexpr int kMaxStepsCounters = 4096;   // counters[step] for main queues; [kMaxStepsCounters + step] shadow
+constexpr int kErrorSlot = 2 * kMaxStepsCounters - 1;   // set by kernels on an internal inconsistency
 
 // Launchers (all asynchronous on `stream`).
 void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream);

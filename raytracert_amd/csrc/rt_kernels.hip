@@ -282,10 +282,11 @@ __device__ __forceinline__ void bvh_query(const DevScene &sc, V3 o, V3 dir, bool
 constexpr int kXcds = 8;
 struct Segment { int begin, end, step, start; };
 __device__ __forceinline__ Segment xcd_segment(int n, int block_dim) {
-    const int xcd = blockIdx.x % kXcds;
-    const int per_xcd_blocks = (gridDim.x + kXcds - 1 - xcd) / kXcds;    // blocks with this residue
-    const int local = blockIdx.x / kXcds;
-    const int chunk = (n + kXcds - 1) / kXcds;
+    const int nseg = min(kXcds, static_cast<int>(gridDim.x));          // every segment gets >= 1 block
+    const int xcd = blockIdx.x % nseg;
+    const int per_xcd_blocks = (static_cast<int>(gridDim.x) - 1 - xcd) / nseg + 1;   // blocks with this residue
+    const int local = blockIdx.x / nseg;
+    const int chunk = (n + nseg - 1) / nseg;
     Segment g;
     g.begin = min(n, xcd * chunk);
     g.end = min(n, g.begin + chunk);
@@ -632,7 +633,11 @@ __global__ __launch_bounds__(kBlock) void k_shade(const DevScene sc, const Shade
     const int lvl = as_int(qd.w);
     if (lvl >= 0) {                                                       // inactive (outside frame) otherwise
         sample = as_int(qo.w);
-        const int idx = w.hit_idx[j];
+        int idx = w.hit_idx[j];
+        if (idx >= sc.nt) {                       // never expected: flag it for the host, do not fault
+            w.counters[kErrorSlot] = 1;
+            idx = -1;
+        }
         const int64_t ci = static_cast<int64_t>(p.step) * w.cap + sample;
         if (idx < 0) {                                                   // trace() miss -> BLACK (:389-391)
             w.chain_local[ci] = make_float4(0, 0, 0, as_float(kChildNone));
