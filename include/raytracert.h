@@ -155,6 +155,11 @@ int rt_scene_bvh_validate(rt_scene *scene);
  * Returns 0 (box written), 1 (ill-conditioned: tested by every query) or 2 (never accepted). */
 int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
 
+/* ---- tuning (launch-shape knobs; results never depend on them) ------------------------- */
+#define RT_TUNE_XCD_SPLIT 0   /* 1: each XCD's blocks take one contiguous segment of a BVH queue */
+#define RT_TUNE_BVH_GRID  1   /* resident grid (blocks of 128 threads) of the BVH kernels */
+int rt_scene_tune(rt_scene *scene, int32_t knob, int32_t value);
+
 /* ---- measurement ---------------------------------------------------------------------- */
 /* Kernel kinds for rt_kernel_stats. */
 #define RT_KERNEL_CLOSEST_HIT 0   /* closest-hit over all triangles (primary + secondary queries) */

@@ -30,6 +30,7 @@ HAS_KD, HAS_KA, HAS_KS, HAS_NS, HAS_NI, HAS_TR, HAS_ILLUM = (1 << i for i in ran
 
 KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME = range(4)
 ACCEL_BRUTE_FORCE, ACCEL_BVH = 0, 1
+TUNE_XCD_SPLIT, TUNE_BVH_GRID = 0, 1
 
 
 class RtParams(C.Structure):
@@ -84,6 +85,7 @@ _SIGNATURES = {
     "rt_scene_bvh_info": ([_VP, _VP], C.c_int),
     "rt_scene_bvh_validate": ([_VP], C.c_int),
     "rt_bvh_acceptance_box": ([_VP, _VP, _VP], C.c_int),
+    "rt_scene_tune": ([_VP, C.c_int32, C.c_int32], C.c_int),
 }
 
 _lib = None

@@ -209,6 +209,11 @@ class Scene:
         return dict(nodes=int(info[0]), depth=int(info[1]), always=int(info[2]), never=int(info[3]),
                     leaf_triangles=int(info[4]))
 
+    def tune(self, knob: str, value: int) -> None:
+        """Launch-shape knobs ('xcd_split', 'bvh_grid'); outputs never depend on them."""
+        k = {"xcd_split": _capi.TUNE_XCD_SPLIT, "bvh_grid": _capi.TUNE_BVH_GRID}[knob]
+        check(lib().rt_scene_tune(self._h, k, int(value)))
+
     def bvh_validate(self) -> None:
         check(lib().rt_scene_bvh_validate(self._h))
 

@@ -52,6 +52,8 @@ struct DevScene {
     int32_t use_bvh, n_always;
     float scene_m1;
     int32_t bvh_depth;              // traversal stack entries needed (tree depth)
+    int32_t xcd_split;              // RT_TUNE_XCD_SPLIT
+    int32_t bvh_grid;               // RT_TUNE_BVH_GRID
     unsigned long long *work;       // BVH kernels' triangle tests / node visits: [0..1] closest-hit, [2..3] shadow
 };
 

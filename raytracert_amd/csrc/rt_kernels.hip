@@ -281,8 +281,8 @@ __device__ __forceinline__ void bvh_query(const DevScene &sc, V3 o, V3 dir, bool
 // the scene it touches small enough to stay in its 4 MB L2. Placement only changes speed.
 constexpr int kXcds = 8;
 struct Segment { int begin, end, step, start; };
-__device__ __forceinline__ Segment xcd_segment(int n, int block_dim) {
-    const int nseg = min(kXcds, static_cast<int>(gridDim.x));          // every segment gets >= 1 block
+__device__ __forceinline__ Segment xcd_segment(int n, int block_dim, bool split) {
+    const int nseg = split ? min(kXcds, static_cast<int>(gridDim.x)) : 1;   // every segment gets >= 1 block
     const int xcd = blockIdx.x % nseg;
     const int per_xcd_blocks = (static_cast<int>(gridDim.x) - 1 - xcd) / nseg + 1;   // blocks with this residue
     const int local = blockIdx.x / nseg;
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_closest_hit(const DevScene sc
     int32_t (*stack)[kBvhBlock] = reinterpret_cast<int32_t (*)[kBvhBlock]>(lds_stack);
     const int n = *q_count;
     unsigned tests = 0, visits = 0;
-    const Segment seg = xcd_segment(n, kBvhBlock);
+    const Segment seg = xcd_segment(n, kBvhBlock, sc.xcd_split != 0);
     for (int base = seg.start; base < seg.end; base += seg.step) {   // resident grid-stride within the XCD's segment
         const int j = base + threadIdx.x;
         bool active = j < seg.end;
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_shadow_hit(const DevScene sc,
     int32_t (*stack)[kBvhBlock] = reinterpret_cast<int32_t (*)[kBvhBlock]>(lds_stack);
     const int n = *q_count;
     unsigned tests = 0, visits = 0;
-    const Segment seg = xcd_segment(n, kBvhBlock);
+    const Segment seg = xcd_segment(n, kBvhBlock, sc.xcd_split != 0);
     for (int base = seg.start; base < seg.end; base += seg.step) {   // resident grid-stride within the XCD's segment
         const int j = base + threadIdx.x;
         const bool active = j < seg.end;
@@ -817,8 +817,8 @@ inline size_t bvh_lds(const DevScene &s) { return sizeof(int32_t) * kBvhBlock * 
 
 // 128-thread blocks with a 10-20 KB LDS stack: 16 resident per CU (32 waves) -> 4096 blocks.
 constexpr int kMaxBvhGrid = 4096;
-inline unsigned grid_bvh(int64_t n) {
-    return static_cast<unsigned>(std::min<int64_t>((n + kBvhBlock - 1) / kBvhBlock, kMaxBvhGrid));
+inline unsigned grid_bvh(int64_t n, int cap = kMaxBvhGrid) {
+    return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n + kBvhBlock - 1) / kBvhBlock, cap)));
 }
 inline unsigned grid_chunked(int64_t n) {
     return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n + kBlock * kPer - 1) / (kBlock * kPer), kMaxGrid)));
@@ -830,7 +830,7 @@ inline unsigned grid_stride(int64_t n) {
 void launch_closest_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
     if (capacity <= 0) return;
     if (s.use_bvh) {
-        hipLaunchKernelGGL(k_bvh_closest_hit, dim3(grid_bvh(capacity)), dim3(kBvhBlock), bvh_lds(s), stream, s,
+        hipLaunchKernelGGL(k_bvh_closest_hit, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s,
                            w.q_org[step & 1], w.q_dst[step & 1], &w.counters[step], w.hit_idx, w.hit_I);
         return;
     }
@@ -848,10 +848,10 @@ void launch_shadow_hit(const DevScene &s, const DevWork &w, int step, int64_t ca
     if (capacity <= 0) return;
     if (s.use_bvh) {
         if (s.any_transparent)
-            hipLaunchKernelGGL(k_bvh_shadow_hit<false>, dim3(grid_bvh(capacity)), dim3(kBvhBlock), bvh_lds(s), stream, s,
+            hipLaunchKernelGGL(k_bvh_shadow_hit<false>, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s,
                                w.sq_org, w.sq_dst, &w.counters[kMaxStepsCounters + step], w.shadow);
         else
-            hipLaunchKernelGGL(k_bvh_shadow_hit<true>, dim3(grid_bvh(capacity)), dim3(kBvhBlock), bvh_lds(s), stream, s,
+            hipLaunchKernelGGL(k_bvh_shadow_hit<true>, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s,
                                w.sq_org, w.sq_dst, &w.counters[kMaxStepsCounters + step], w.shadow);
         return;
     }
@@ -884,7 +884,7 @@ void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *d
                            float4 *I, hipStream_t stream) {
     if (n <= 0) return;
     if (s.use_bvh) {
-        hipLaunchKernelGGL(k_bvh_intersect_only, dim3(grid_bvh(n)), dim3(kBvhBlock), bvh_lds(s), stream, s, org, dst, n, idx, I);
+        hipLaunchKernelGGL(k_bvh_intersect_only, dim3(grid_bvh(n, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, org, dst, n, idx, I);
         return;
     }
     hipLaunchKernelGGL(k_intersect_only, dim3(grid_for(n)), dim3(kBlock), 0, stream, s.tris, s.nt, org, dst, n, idx, I);

@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""A/B launch-shape variants on the benchmark frame in ONE process (interleaved rounds), reporting
+per-kernel milliseconds from HIP events (cdna_hip_programming.md §5.4 rule 24)."""
+import json
+import os
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401
+
+import raytracert_amd as R  # noqa: E402
+from raytracert_amd import scenes  # noqa: E402
+from raytracert_amd._capi import KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME  # noqa: E402
+
+variants = json.loads(sys.argv[1]) if len(sys.argv) > 1 else [{}]
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+spec = getattr(scenes, sys.argv[3]) if len(sys.argv) > 3 else scenes.C4
+obj = scenes.write_sphere_grid(spec, tempfile.mkdtemp(), "ab")
+sc = R.Scene.load(obj, device=0)
+p = R.RenderParams(width=1920, height=1080, pf=1, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
+ref, _, _ = sc.render(p)
+res = {i: [] for i in range(len(variants))}
+for r in range(rounds):
+    for i, v in enumerate(variants):
+        for k, val in v.items():
+            sc.tune(k, val)
+        sc.reset_stats()
+        sc.set_profiling(True)
+        u8, _, _ = sc.render(p)
+        sc.set_profiling(False)
+        assert np.array_equal(u8, ref), f"variant {v} changed the image"
+        res[i].append({name: sc.kernel_stats(k)[1] for name, k in
+                       (("ch", KERNEL_CLOSEST_HIT), ("shadow", KERNEL_SHADOW), ("shade", KERNEL_SHADE), ("frame", KERNEL_FRAME))})
+for i, v in enumerate(variants):
+    med = {k: float(np.median([x[k] for x in res[i]])) for k in res[i][0]}
+    tot = sum(med.values())
+    print(json.dumps({"variant": v, "median_ms": {k: round(x, 3) for k, x in med.items()}, "total_ms": round(tot, 3)}))
