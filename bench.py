@@ -32,9 +32,37 @@ FLOP_PER_TEST = 37            # fp32 ops of rayIntersectTriangle
 FLOP_PER_NODE = 52            # BVH node visit: 2 slab tests (6 sub + 6 mul + 12 min/max each) + 2 distance culls
 FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector (= FP32 matrix) peak
 HBM_PEAK_GBS = 8000.0
-WIDTH, HEIGHT, PF, MAX_LVL = 1920, 1080, 1, 3
-LIGHTS = ((0.0, 0.0, 4.0), (1.5, 1.5, 4.0))
 TILE = 16
+# BASELINE.json configs. C4 is the metric's configuration and the default; the
+# others are available with --workload (C1 is the reference's own CPU-only plumbing case).
+WORKLOADS = {
+    "c4": dict(desc="C4: synthetic 8x8 UV-sphere grid OBJ (102,402 tris) 1920x1080, pf 1, depth 3, 2 lights",
+               scene="syn:C4", width=1920, height=1080, pf=1, max_lvl=3, lights=((0.0, 0.0, 4.0), (1.5, 1.5, 4.0))),
+    "c2": dict(desc="C2: dodgeColorTest.obj (16,311 tris) 800x600, pf 1, depth 1, 1 light",
+               scene="ref:dodgeColorTest.obj", width=800, height=600, pf=1, max_lvl=1, lights=((0.0, 0.0, 4.0),)),
+    "c3": dict(desc="C3: Balls surrogate (3 UV spheres 48x24 + ground quad, Balls.mtl materials) 1920x1080, pf 1, "
+                    "depth 3, 2 lights (Balls.obj is missing from the reference)",
+               scene="syn:balls", width=1920, height=1080, pf=1, max_lvl=3, lights=((0.0, 0.0, 4.0), (2.0, 2.0, 4.0))),
+    "c5": dict(desc="C5: synthetic 16x16 UV-sphere grid OBJ (1,015,810 tris) 3840x2160, pf 2 (4 samples/pixel, "
+                    "the reference's regular AA grid), depth 3, 4 lights",
+               scene="syn:C5", width=3840, height=2160, pf=2, max_lvl=3,
+               lights=((0.0, 0.0, 4.0), (1.5, 1.5, 4.0), (-1.5, 1.5, 4.0), (0.0, -1.5, 4.0))),
+}
+
+
+def workload_scene(spec, workdir):
+    """Scene file for a workload: synthetic scenes are regenerated; reference models come from the
+    gzip'd data fixtures in tests/golden/models (the reference tree is not on the GPU box)."""
+    from raytracert_amd import scenes
+    kind, name = spec.split(":", 1)
+    if kind == "syn":
+        if name == "balls":
+            return scenes.balls_surrogate(workdir)
+        return scenes.write_sphere_grid(getattr(scenes, name), workdir, name.lower())
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    from _util import materialize_models
+    materialize_models(workdir)
+    return os.path.join(workdir, name)
 
 
 def parse():
@@ -49,6 +77,7 @@ def parse():
     ap.add_argument("--profile-steps", type=int, default=1, help="steps re-run with HIP events for the roofline")
     ap.add_argument("--ppm", default="", help="write the first frame to this PPM (rank 0)")
     ap.add_argument("--accel", choices=("bvh", "brute_force"), default="bvh")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c4")
     ap.add_argument("--no-bf-roofline", action="store_true", help="skip the brute-force kernel's roofline frame")
     return ap.parse_args()
 
@@ -78,9 +107,11 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
+    wl = WORKLOADS[args.workload]
+    WIDTH, HEIGHT, PF, MAX_LVL, LIGHTS = wl["width"], wl["height"], wl["pf"], wl["max_lvl"], wl["lights"]
     tmp = tempfile.mkdtemp(prefix=f"rtbench_r{rank}_")
     t_gen = time.time()
-    obj = scenes.write_sphere_grid(scenes.C4, tmp, "c4_sphere_grid")
+    obj = workload_scene(wl["scene"], tmp)
     t_gen = time.time() - t_gen
     t_load = time.time()
     scene = R.Scene.load(obj, device=local_rank)
@@ -95,20 +126,14 @@ def main():
     plan = rdist.ShardPlan(layout, world, frames=world if args.mode == "weak" else 1)
     buf = torch.zeros(plan.shard_bytes, dtype=torch.uint8, device=dev)
     index = torch.as_tensor(plan.gather_index(), device=dev)
-    calls = plan.calls(rank)
     stream = torch.cuda.current_stream(dev)
 
     def render_shard(want_counts=False):
-        off = 0
-        counts = np.zeros(3, np.uint64)
-        for (_, first, stride) in calls:
-            n_cap = (buf.numel() - off)
-            n, c = scene.render_tiles_device(cparams, TILE, TILE, first, stride, buf.data_ptr() + off, n_cap,
-                                             stream.cuda_stream, want_counts=want_counts)
-            off += n * layout.tile_bytes
-            if c is not None:
-                counts += c
-        return counts
+        # one call: this rank's tile ids rank, rank + N, ... over the step's `frames` frames
+        n, c = scene.render_tiles_device(cparams, TILE, TILE, rank, world, buf.data_ptr(), buf.numel(),
+                                         stream.cuda_stream, want_counts=want_counts, frames=plan.frames)
+        assert n == plan.rank_tiles(rank)
+        return c if c is not None else np.zeros(3, np.uint64)
 
     def step():
         render_shard()
@@ -180,17 +205,22 @@ def main():
         value = total_rays / elapsed / 1e6
         queries = ch_tests / max(nt, 1)
         if args.accel == "bvh":
-            # work actually done: triangle tests + node visits (device counters)
+            # BVH traversal is a dependent gather: per query 32 B in + 20 B out, plus one 64-B
+            # record per node visit and per triangle test (device counters). Roof: memory (HBM peak).
             kname = "k_bvh_closest_hit"
             flops = bvh_tests * FLOP_PER_TEST + bvh_visits * FLOP_PER_NODE
-            # per query: 32 B in + 20 B out, and 64 B per node visit and per triangle test (L2-served)
             ch_bytes = queries * 52.0 + (bvh_visits + bvh_tests) * 64.0
+            bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
+            achieved = ch_bytes / (ch_ms / 1e3) / 1e9 if ch_ms > 0 else 0.0
+            valu = flops / (ch_ms / 1e3) / 1e12 if ch_ms > 0 else 0.0
         else:
+            # brute force: each wave streams every 64-B record once (scalar loads); VALU-bound
             kname = "k_closest_hit"
             flops = ch_tests * FLOP_PER_TEST
-            # each wave streams every 64-B triangle record once (scalar loads); queries 52 B each
             ch_bytes = ch_tests / 64.0 * 64.0 + queries * 52.0
-        achieved = flops / (ch_ms / 1e3) / 1e12 if ch_ms > 0 else 0.0
+            bound, unit, peak = "valu", "TFLOP/s", FP32_PEAK_TFLOPS
+            achieved = flops / (ch_ms / 1e3) / 1e12 if ch_ms > 0 else 0.0
+            valu = achieved
         traffic, traffic_src = pmc_traffic(kname)
         result = {
             "metric": METRIC,
@@ -206,7 +236,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "workload": "C4: synthetic 8x8 UV-sphere grid OBJ (102,402 tris) 1920x1080, pf 1, depth 3, 2 lights",
+                "workload": wl["desc"],
                 "frames_per_step": plan.frames,
                 "width": WIDTH, "height": HEIGHT, "pf": PF, "max_lvl": MAX_LVL, "lights": [list(l) for l in LIGHTS],
                 "triangles": nt, "vertices": nv, "tile": TILE,
@@ -218,11 +248,14 @@ def main():
             },
             "roofline": {
                 "kernel": f"{kname} (primary + secondary queries, accel={args.accel})",
-                "bound": "valu",
+                "bound": bound,
                 "achieved": round(achieved, 3),
-                "peak": FP32_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                "peak": peak,
+                "unit": unit,
+                "frac": round(achieved / peak, 4),
+                "algorithmic_bytes_per_launch": round(ch_bytes / max(ch_launches, 1)),
+                "valu_TFLOPs": round(valu, 3),
+                "valu_frac": round(valu / FP32_PEAK_TFLOPS, 4),
                 "traffic": traffic,
                 "traffic_unit": "bytes/launch (PMC: 2*FETCH_SIZE + WRITE_SIZE)",
                 "traffic_source": traffic_src,
@@ -234,8 +267,6 @@ def main():
                 "flop_per_test": FLOP_PER_TEST,
                 "flop_per_node_visit": FLOP_PER_NODE,
                 "bruteforce_equivalent_TFLOPs": round(ch_tests * FLOP_PER_TEST / (ch_ms / 1e3) / 1e12, 3) if ch_ms > 0 else None,
-                "hbm_algorithmic_GBps": round(ch_bytes / (ch_ms / 1e3) / 1e9, 2) if ch_ms > 0 else None,
-                "hbm_peak_GBps": HBM_PEAK_GBS,
             },
             "kernel_ms_per_step": {
                 "closest_hit": round(ch_ms / max(args.profile_steps, 1), 3),
@@ -252,7 +283,7 @@ def main():
 
     # ---- CPU baseline + in-run parity on a bounded tile sample (rank 0, N=1 only) ----
     if rank == 0 and world == 1 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(obj, params, frames[0].cpu().numpy(), layout, args)
+        result["cpu_baseline"] = cpu_baseline(obj, params, frames[0].cpu().numpy(), layout, args, wl)
 
     if world > 1:
         dist.barrier()
@@ -277,7 +308,7 @@ def pmc_traffic(kernel: str):
     return None, None
 
 
-def cpu_baseline(obj, params, gpu_frame, layout, args):
+def cpu_baseline(obj, params, gpu_frame, layout, args, wl):
     """Time the CPU restatement (oracle/, 'port') on every k-th 16x16 tile of the same frame with
     --cpu-threads threads, and check the GPU's bytes on those tiles against it."""
     import numpy as np
@@ -315,7 +346,7 @@ def cpu_baseline(obj, params, gpu_frame, layout, args):
         "cores": threads,
         "kind": "port",
         "sample": f"{len(tiles)} of {layout.n_tiles} 16x16 tiles (every {args.cpu_sample_every}th) of the same "
-                  f"C4 frame, {rays} rays in {dt:.1f} s, oracle/rt_oracle.c (-O2) on {threads} threads, "
+                  f"{wl['desc'].split(':')[0]} frame, {rays} rays in {dt:.1f} s, oracle/rt_oracle.c (-O2) on {threads} threads, "
                   f"host {platform.processor() or platform.machine()}",
         "parity_vs_gpu": {"bytes": total, "exact_frac": round(exact / max(total, 1), 6), "max_lsb": max_d},
     }

@@ -122,13 +122,14 @@ int rt_trace_rays(rt_scene *scene, const rt_params *params, const float *origins
 int rt_render_tile(rt_scene *scene, const rt_params *params, int32_t x0, int32_t y0, int32_t w, int32_t h,
                    uint8_t *rgb_u8, float *rgb_f32, uint64_t counts[3]);
 /* Interleaved tile shard for multi-GPU rendering, fully device-resident. The frame is cut into
- * tile_w x tile_h tiles numbered row-major (tiles_x = ceil(width/tile_w)); this call renders tiles
- * first, first+stride, first+2*stride, ... and writes each as tile_w*tile_h*3 bytes (pixels outside
- * the frame are 0) into the DEVICE buffer d_out_u8 in that order. stream is a hipStream_t (NULL =
- * the scene's own stream); the call returns after enqueueing (no host synchronisation) unless
- * counts != NULL. Returns the number of tiles written via n_tiles_out. */
+ * tile_w x tile_h tiles numbered row-major (tiles_x = ceil(width/tile_w), T tiles per frame); a batch
+ * of `frames` frames of this view has tile ids g = f*T + t. This call renders ids first,
+ * first+stride, first+2*stride, ... below frames*T and writes each as tile_w*tile_h*3 bytes (pixels
+ * outside the frame are 0) into the DEVICE buffer d_out_u8 in that order. stream is a hipStream_t
+ * (NULL = the scene's own stream); the call returns after enqueueing (no host synchronisation)
+ * unless counts != NULL. Returns the number of tiles written via n_tiles_out. */
 int rt_render_tiles_device(rt_scene *scene, const rt_params *params, int32_t tile_w, int32_t tile_h,
-                           int32_t first, int32_t stride, void *d_out_u8, size_t out_capacity,
+                           int32_t frames, int32_t first, int32_t stride, void *d_out_u8, size_t out_capacity,
                            void *stream, int32_t *n_tiles_out, uint64_t counts[3]);
 
 /* ---- helpers -------------------------------------------------------------------------- */

@@ -72,8 +72,8 @@ _SIGNATURES = {
     "rt_intersect_mesh": ([_VP, _VP, _VP, C.c_int32, _VP, _VP], C.c_int),
     "rt_trace_rays": ([_VP, C.POINTER(RtParams), _VP, _VP, C.c_int32, _VP, _VP], C.c_int),
     "rt_render_tile": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP, _VP, _VP], C.c_int),
-    "rt_render_tiles_device": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP, C.c_size_t,
-                                _VP, C.POINTER(C.c_int32), _VP], C.c_int),
+    "rt_render_tiles_device": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP,
+                                C.c_size_t, _VP, C.POINTER(C.c_int32), _VP], C.c_int),
     "rt_default_corners": ([C.c_int32, C.c_int32, _VP], C.c_int),
     "rt_write_ppm": ([C.c_char_p, C.c_int32, C.c_int32, _VP], C.c_int),
     "rt_set_profiling": ([_VP, C.c_int32], C.c_int),

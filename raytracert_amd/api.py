@@ -182,12 +182,14 @@ class Scene:
         return u8, f32, counts
 
     def render_tiles_device(self, params: RenderParams | RtParams, tile_w: int, tile_h: int, first: int, stride: int,
-                            out_ptr: int, out_capacity: int, stream_ptr: int | None = None, want_counts: bool = False):
-        """Interleaved tile shard into a device buffer (e.g. a torch uint8 CUDA tensor's data_ptr())."""
+                            out_ptr: int, out_capacity: int, stream_ptr: int | None = None, want_counts: bool = False,
+                            frames: int = 1):
+        """Interleaved tile shard (ids first, first+stride, ... over `frames` frames of this view) into a
+        device buffer, e.g. a torch uint8 CUDA tensor's data_ptr()."""
         p = params.to_c() if isinstance(params, RenderParams) else params
         n_tiles = C.c_int32()
         counts = np.zeros(3, np.uint64) if want_counts else None
-        check(lib().rt_render_tiles_device(self._h, C.byref(p), tile_w, tile_h, first, stride, C.c_void_p(out_ptr),
+        check(lib().rt_render_tiles_device(self._h, C.byref(p), tile_w, tile_h, frames, first, stride, C.c_void_p(out_ptr),
                                            out_capacity, C.c_void_p(stream_ptr) if stream_ptr else None,
                                            C.byref(n_tiles), _ptr(counts)))
         return n_tiles.value, counts

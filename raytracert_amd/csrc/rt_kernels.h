@@ -22,7 +22,7 @@ struct FrameGeom {
     int32_t tile0, ntiles;              // this batch
     int32_t ox, oy, cw, ch;             // tiled region origin / clip size (absolute pixels)
     int32_t out_mode;                   // 0: tile-major shard layout, 1: row-major in the clip rect
-    int32_t pad;
+    int32_t tiles_total;                // tiles per frame: ids wrap modulo this (multi-frame batches)
     float corners[8][3];                // origin00,dest00,origin01,dest01,origin10,dest10,origin11,dest11
 };
 

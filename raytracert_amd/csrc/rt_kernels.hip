@@ -480,7 +480,7 @@ __device__ __forceinline__ bool decode_pixel(const FrameGeom &g, int64_t pix, in
     const int tpx = g.tw * g.th;
     const int tl = static_cast<int>(pix / tpx);
     const int p = static_cast<int>(pix - static_cast<int64_t>(tl) * tpx);
-    const int tid = g.first + (g.tile0 + tl) * g.stride;
+    const int tid = (g.first + (g.tile0 + tl) * g.stride) % g.tiles_total;
     const int tx = tid % g.tiles_x, ty = tid / g.tiles_x;
     x = g.ox + tx * g.tw + (p % g.tw);
     y = g.oy + ty * g.th + (p / g.tw);

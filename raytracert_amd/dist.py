@@ -155,6 +155,11 @@ class ShardPlan:
         T = self.layout.n_tiles
         return (T - first + self.world - 1) // self.world if first < T else 0
 
+    def rank_tiles(self, rank: int) -> int:
+        """Tiles rank holds: ids rank, rank + world, ... below frames * T (one rt_render_tiles_device
+        call with frames=self.frames, first=rank, stride=world)."""
+        return (self.total_tiles - rank + self.world - 1) // self.world if rank < self.total_tiles else 0
+
     def gather_index(self):
         """index[g] = position of global tile g in the gathered [world * slots] tile array."""
         g = np.arange(self.total_tiles, dtype=np.int64)

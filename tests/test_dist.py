@@ -41,10 +41,11 @@ def _worker(rank, world, port, mode, result_path):
     plan = rdist.ShardPlan(layout, world, frames=world if mode == "weak" else 1)
     buf = torch.zeros(plan.shard_bytes, dtype=torch.uint8)
     off = 0
-    for (_, first, stride) in plan.calls(rank):
+    for (_, first, stride) in plan.calls(rank):   # == one multi-frame call: ids rank, rank+world, ...
         t = stub_render(layout, first, stride).reshape(-1)
         buf[off:off + t.size] = torch.from_numpy(t)
         off += t.size
+    assert off == plan.rank_tiles(rank) * layout.tile_bytes
     gathered = rdist.gather_shards(buf, rank, world)
     if rank == 0:
         frames = rdist.assemble_plan_torch(gathered, plan).numpy()

@@ -237,3 +237,29 @@ def test_c4_full_frame_bvh_equals_brute_force(workdir, gpu_available):
     assert [int(x) for x in ac] == [int(x) for x in bc]
     assert np.array_equal(a, b)
     assert np.array_equal(af.view(np.uint32), bf.view(np.uint32))
+
+
+def test_multi_frame_shard_batch_reassembles(workdir, gpu_available):
+    """Weak-scaling step shape: a batch of 3 frames of one view, ids g = f*T + t interleaved over 3
+    ranks, one rt_render_tiles_device call per rank; every assembled frame equals the render."""
+    import torch
+    from raytracert_amd import dist
+    path = scene_path("syn:F3", workdir)
+    p = R.RenderParams(width=100, height=70, pf=1, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
+    layout = dist.TileLayout(p.width, p.height, 16, 16)
+    plan = dist.ShardPlan(layout, 3, frames=3)
+    with R.Scene.load(path, device=0) as sc:
+        full, _, counts = sc.render(p)
+        shards = []
+        total = np.zeros(3, np.uint64)
+        for rank in range(3):
+            buf = torch.zeros(plan.shard_bytes, dtype=torch.uint8, device="cuda:0")
+            n, c = sc.render_tiles_device(p, 16, 16, rank, 3, buf.data_ptr(), buf.numel(),
+                                          torch.cuda.current_stream().cuda_stream, want_counts=True, frames=3)
+            assert n == plan.rank_tiles(rank)
+            total += c
+            shards.append(buf)
+        frames = dist.assemble_plan_torch(torch.cat(shards), plan).cpu().numpy()
+    for f in frames:
+        assert np.array_equal(f, full)
+    assert [int(x) for x in total] == [3 * int(x) for x in counts]
