@@ -180,7 +180,15 @@ def main():
         torch.cuda.synchronize(dev)
         scene.set_profiling(False)
         st = {k: scene.kernel_stats(k) for k in (KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME)}
-        work = scene.work_stats(KERNEL_CLOSEST_HIT) if scene.accel() == "bvh" else (0.0, 0.0)
+        work = (0.0, 0.0)
+        if scene.accel() == "bvh":   # work counters slow the kernels: count in a separate, untimed pass
+            scene.reset_stats()
+            scene.set_profiling(True, count_work=True)
+            for _ in range(max(steps, 1)):
+                render_shard()
+            torch.cuda.synchronize(dev)
+            scene.set_profiling(False)
+            work = scene.work_stats(KERNEL_CLOSEST_HIT)
         return st, work
 
     stats, (bvh_tests, bvh_visits) = profile(args.profile_steps)

@@ -147,9 +147,11 @@ int rt_write_ppm(const char *path, int32_t width, int32_t height, const uint8_t 
 #define RT_ACCEL_BVH         1
 int rt_scene_set_accel(rt_scene *scene, int32_t mode);
 int rt_scene_get_accel(const rt_scene *scene, int32_t *mode);
-/* info[0] inner nodes, [1] depth, [2] always-tested (ill-conditioned) triangles, [3] never-accepted
- * (degenerate) triangles, [4] triangles in leaves. Builds the BVH on demand. */
-int rt_scene_bvh_info(rt_scene *scene, int32_t info[5]);
+/* info[0] inner nodes of the binary tree, [1] its depth, [2] always-tested (ill-conditioned)
+ * triangles, [3] never-accepted (degenerate) triangles, [4] triangles in leaves, [5] nodes of the
+ * four-wide tree the kernels traverse by default, [6] its depth. Builds the BVH on demand. */
+#define RT_BVH_INFO_FIELDS 7
+int rt_scene_bvh_info(rt_scene *scene, int32_t info[RT_BVH_INFO_FIELDS]);
 /* Host-side structural check of the built BVH (containment, coverage, depth bound). */
 int rt_scene_bvh_validate(rt_scene *scene);
 /* The padded acceptance box of one triangle T = {T0, T1, T2} (9 floats), as the BVH uses it.
@@ -157,8 +159,11 @@ int rt_scene_bvh_validate(rt_scene *scene);
 int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
 
 /* ---- tuning (launch-shape knobs; results never depend on them) ------------------------- */
-#define RT_TUNE_XCD_SPLIT 0   /* 1: each XCD's blocks take one contiguous segment of a BVH queue */
+#define RT_TUNE_XCD_SPLIT 0   /* BVH queue distribution: 0 grid-stride, 1 one static segment per XCD,
+                                 2 per-XCD segments with work-stealing wave counters */
 #define RT_TUNE_BVH_GRID  1   /* resident grid (blocks of 128 threads) of the BVH kernels */
+#define RT_TUNE_BVH_WIDTH 2   /* 4 (default): quantised four-wide nodes; 2: float binary nodes */
+#define RT_TUNE_LDS_STACK 3   /* traversal stack entries per lane kept in LDS; deeper ones in HBM */
 int rt_scene_tune(rt_scene *scene, int32_t knob, int32_t value);
 
 /* ---- measurement ---------------------------------------------------------------------- */
@@ -168,15 +173,26 @@ int rt_scene_tune(rt_scene *scene, int32_t knob, int32_t value);
 #define RT_KERNEL_SHADE       2   /* shading / secondary-ray generation */
 #define RT_KERNEL_FRAME       3   /* sample generation + fold + AA + quantise */
 #define RT_KERNEL_KINDS       4
-/* When enabled, every launch of the scene is bracketed with hipEvents on its own stream and the
- * durations accumulated (one host sync per render call). */
-int rt_set_profiling(rt_scene *scene, int32_t enabled);
+/* RT_PROFILE_TIMING: every launch of the scene is bracketed with hipEvents on its own stream and
+ * the durations accumulated (one host sync per render call). RT_PROFILE_WORK additionally has the
+ * BVH kernels count their work (rt_work_stats / rt_work_detail); the counting itself costs time,
+ * so time and count in separate passes. */
+#define RT_PROFILE_OFF    0
+#define RT_PROFILE_TIMING 1
+#define RT_PROFILE_WORK   2
+int rt_set_profiling(rt_scene *scene, int32_t mode);
 /* launches, summed milliseconds, and summed ray-triangle tests (closest-hit/shadow kinds). */
 int rt_kernel_stats(rt_scene *scene, int32_t kind, uint64_t *launches, double *total_ms, double *tests);
 int rt_reset_stats(rt_scene *scene);
 /* Ray-triangle tests and BVH node visits executed by the BVH kernels of `kind`
- * (RT_KERNEL_CLOSEST_HIT or RT_KERNEL_SHADOW) since the last reset (synchronises the device). */
+ * (RT_KERNEL_CLOSEST_HIT or RT_KERNEL_SHADOW) while profiling was RT_PROFILE_WORK, since the last
+ * reset (synchronises the device). */
 int rt_work_stats(rt_scene *scene, int32_t kind, double *tests, double *node_visits);
+/* The same counters in full: [0] tests, [1] node visits, [2] sum over wave tasks (64 queries side
+ * by side) of the largest per-query visit count, [3] largest visit count of any query, [4] wave
+ * tasks, [5] sum over wave tasks of the largest per-query test count. */
+#define RT_WORK_FIELDS 6
+int rt_work_detail(rt_scene *scene, int32_t kind, uint64_t out[RT_WORK_FIELDS]);
 
 #ifdef __cplusplus
 }

@@ -30,7 +30,9 @@ HAS_KD, HAS_KA, HAS_KS, HAS_NS, HAS_NI, HAS_TR, HAS_ILLUM = (1 << i for i in ran
 
 KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME = range(4)
 ACCEL_BRUTE_FORCE, ACCEL_BVH = 0, 1
-TUNE_XCD_SPLIT, TUNE_BVH_GRID = 0, 1
+TUNE_XCD_SPLIT, TUNE_BVH_GRID, TUNE_BVH_WIDTH, TUNE_LDS_STACK = 0, 1, 2, 3
+BVH_INFO_FIELDS = 7
+WORK_FIELDS = 6
 
 
 class RtParams(C.Structure):
@@ -83,6 +85,7 @@ _SIGNATURES = {
     "rt_scene_set_accel": ([_VP, C.c_int32], C.c_int),
     "rt_scene_get_accel": ([_VP, C.POINTER(C.c_int32)], C.c_int),
     "rt_scene_bvh_info": ([_VP, _VP], C.c_int),
+    "rt_work_detail": ([_VP, C.c_int32, _VP], C.c_int),
     "rt_scene_bvh_validate": ([_VP], C.c_int),
     "rt_bvh_acceptance_box": ([_VP, _VP, _VP], C.c_int),
     "rt_scene_tune": ([_VP, C.c_int32, C.c_int32], C.c_int),

@@ -206,22 +206,27 @@ class Scene:
         return "bvh" if m.value == _capi.ACCEL_BVH else "brute_force"
 
     def bvh_info(self) -> dict:
-        info = np.zeros(5, np.int32)
+        info = np.zeros(_capi.BVH_INFO_FIELDS, np.int32)
         check(lib().rt_scene_bvh_info(self._h, _ptr(info)))
         return dict(nodes=int(info[0]), depth=int(info[1]), always=int(info[2]), never=int(info[3]),
-                    leaf_triangles=int(info[4]))
+                    leaf_triangles=int(info[4]), nodes4=int(info[5]), depth4=int(info[6]))
 
     def tune(self, knob: str, value: int) -> None:
-        """Launch-shape knobs ('xcd_split', 'bvh_grid'); outputs never depend on them."""
-        k = {"xcd_split": _capi.TUNE_XCD_SPLIT, "bvh_grid": _capi.TUNE_BVH_GRID}[knob]
+        """Launch-shape knobs ('xcd_split', 'bvh_grid', 'bvh_width', 'lds_stack'); outputs never
+        depend on them."""
+        k = {"xcd_split": _capi.TUNE_XCD_SPLIT, "bvh_grid": _capi.TUNE_BVH_GRID,
+             "bvh_width": _capi.TUNE_BVH_WIDTH, "lds_stack": _capi.TUNE_LDS_STACK}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
 
     def bvh_validate(self) -> None:
         check(lib().rt_scene_bvh_validate(self._h))
 
     # -- measurement -------------------------------------------------------------------------
-    def set_profiling(self, enabled: bool) -> None:
-        check(lib().rt_set_profiling(self._h, 1 if enabled else 0))
+    def set_profiling(self, enabled: bool | int, count_work: bool = False) -> None:
+        """Time every launch (HIP events); with count_work the BVH kernels also count their work
+        (rt_work_detail), which slows them: time and count in separate passes."""
+        mode = 0 if not enabled else (2 if count_work else 1)
+        check(lib().rt_set_profiling(self._h, mode))
 
     def kernel_stats(self, kind: int) -> tuple[int, float, float]:
         launches, ms, tests = C.c_uint64(), C.c_double(), C.c_double()
@@ -237,6 +242,17 @@ class Scene:
         t, v = C.c_double(), C.c_double()
         check(lib().rt_work_stats(self._h, kind, C.byref(t), C.byref(v)))
         return t.value, v.value
+
+    def work_detail(self, kind: int = _capi.KERNEL_CLOSEST_HIT) -> dict:
+        """Full BVH work counters of `kind` (rt_work_detail): tests, visits, the per-wave-task
+        maxima that give the traversal's SIMD efficiency, the longest query."""
+        d = np.zeros(_capi.WORK_FIELDS, np.uint64)
+        check(lib().rt_work_detail(self._h, kind, _ptr(d)))
+        keys = ("tests", "visits", "wave_max_visits", "max_visits", "wave_tasks", "wave_max_tests")
+        out = {k: int(x) for k, x in zip(keys, d)}
+        out["simd_eff_visits"] = out["visits"] / max(1, 64 * out["wave_max_visits"])
+        out["simd_eff_tests"] = out["tests"] / max(1, 64 * out["wave_max_tests"])
+        return out
 
 
 def bvh_acceptance_box(T) -> tuple[int, np.ndarray, np.ndarray]:

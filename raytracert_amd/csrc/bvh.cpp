@@ -158,7 +158,99 @@ struct Builder {
     }
 };
 
+
+int32_t leaf_ref(const BuildNode &bn) {
+    return static_cast<int32_t>(kBvhLeafBit | (static_cast<uint32_t>(bn.count) << kBvhCountShift) | static_cast<uint32_t>(bn.first));
+}
+
+// Quantise axis k of up to four child boxes in the frame [L, H]: the smallest exponent for which
+// every decoded bound lands on the outside of the float bound it replaces.
+bool quantize_axis(float L, float H, const Box *boxes, int nc, int k, Bvh4Node &g) {
+    const double ext = double(H) - double(L);
+    int e = -126;
+    if (ext > 0) e = std::max(-126, static_cast<int>(std::ceil(std::log2(ext / 255.0))) - 1);
+    for (; e <= 100; ++e) {
+        if (bvh4_decode(L, e, 255) < H) continue;
+        const double scale = std::ldexp(1.0, e);
+        uint32_t lo = 0, hi = 0;
+        bool ok = true;
+        for (int c = 0; c < nc && ok; ++c) {
+            const float cl = boxes[c].lo[k], ch = boxes[c].hi[k];
+            int ql = static_cast<int>(std::min(255.0, std::max(0.0, std::floor((double(cl) - L) / scale))));
+            while (ql > 0 && bvh4_decode(L, e, ql) > cl) --ql;
+            int qh = static_cast<int>(std::min(255.0, std::max(0.0, std::ceil((double(ch) - L) / scale))));
+            while (qh < 255 && bvh4_decode(L, e, qh) < ch) ++qh;
+            ok = bvh4_decode(L, e, ql) <= cl && bvh4_decode(L, e, qh) >= ch;
+            lo |= static_cast<uint32_t>(ql) << (8 * c);
+            hi |= static_cast<uint32_t>(qh) << (8 * c);
+        }
+        if (!ok) continue;
+        g.ex[k] = static_cast<int8_t>(e);
+        g.qlo[k] = lo;
+        g.qhi[k] = hi;
+        return true;
+    }
+    return false;
+}
+
+bool make_node4(const Box *boxes, const int32_t *refs, int nc, Bvh4Node &g) {
+    g = Bvh4Node{};
+    Box u;
+    for (int c = 0; c < nc; ++c) u.grow(boxes[c]);
+    g.n_children = static_cast<uint8_t>(nc);
+    for (int c = 0; c < 4; ++c) g.child[c] = c < nc ? refs[c] : kBvhEmpty;
+    for (int k = 0; k < 3; ++k) {
+        g.origin[k] = nc ? u.lo[k] : 0.0f;
+        if (nc == 0) continue;
+        if (!quantize_axis(u.lo[k], u.hi[k], boxes, nc, k, g)) return false;
+    }
+    return true;
+}
+
+// Collapse the binary build tree into four-wide nodes: repeatedly open the largest-area inner
+// child until a node has four children (the usual SAH-driven collapse), depth-first order.
+struct Collapser {
+    const Builder &b;
+    std::vector<Bvh4Node> &out;
+    int depth = 0;
+    bool ok = true;
+    int run(int n, int level) {
+        std::vector<int> ch{b.nodes[n].left, b.nodes[n].right};
+        while (ch.size() < 4) {
+            int best = -1;
+            double best_area = -1;
+            for (size_t i = 0; i < ch.size(); ++i) {
+                const BuildNode &c = b.nodes[ch[i]];
+                if (c.left >= 0 && c.box.area() > best_area) { best_area = c.box.area(); best = static_cast<int>(i); }
+            }
+            if (best < 0) break;
+            const int x = ch[best];
+            ch[best] = b.nodes[x].left;
+            ch.insert(ch.begin() + best + 1, b.nodes[x].right);
+        }
+        const int id = static_cast<int>(out.size());
+        out.emplace_back();
+        depth = std::max(depth, level);
+        Box boxes[4];
+        int32_t refs[4];
+        const int nc = static_cast<int>(ch.size());
+        for (int c = 0; c < nc; ++c) {
+            const BuildNode &cn = b.nodes[ch[c]];
+            boxes[c] = cn.box;
+            refs[c] = cn.left >= 0 ? run(ch[c], level + 1) : leaf_ref(cn);
+        }
+        Bvh4Node g;
+        ok = ok && make_node4(boxes, refs, nc, g);
+        out[id] = g;
+        return id;
+    }
+};
+
 }  // namespace
+
+float bvh4_decode(float origin, int ex, uint32_t q) {
+    return origin + static_cast<float>(q) * std::ldexp(1.0f, ex);   // q * 2^ex is exact
+}
 
 // Padded acceptance box of one record; returns false if the triangle must be tested by every
 // query (ill-conditioned), and sets *never if it can never be accepted (n == 0).
@@ -215,6 +307,9 @@ int build_bvh(const HostScene &s, const std::vector<TriRec> &recs, HostBvh &out)
         root.c0 = root.c1 = kBvhEmpty;
         out.nodes.push_back(root);
         out.depth = 1;
+        out.nodes4.emplace_back();
+        make_node4(nullptr, nullptr, 0, out.nodes4[0]);
+        out.depth4 = 1;
         return RT_OK;
     }
     b.build(0, np, 0);
@@ -237,14 +332,22 @@ int build_bvh(const HostScene &s, const std::vector<TriRec> &recs, HostBvh &out)
         st.push_back(b.nodes[n].right);
         st.push_back(b.nodes[n].left);
     }
-    auto ref_of = [&](int n) -> int32_t {
-        const BuildNode &bn = b.nodes[n];
-        if (bn.left >= 0) return gpu_id[n];
-        return static_cast<int32_t>(kBvhLeafBit | (static_cast<uint32_t>(bn.count) << kBvhCountShift) | static_cast<uint32_t>(bn.first));
-    };
+    auto ref_of = [&](int n) -> int32_t { return b.nodes[n].left >= 0 ? gpu_id[n] : leaf_ref(b.nodes[n]); };
     if (np >= (1 << kBvhCountShift)) return RT_E_ARG;   // leaf first-index field overflow
     for (const BuildNode &bn : b.nodes)
         if (bn.left < 0 && static_cast<uint32_t>(bn.count) > kBvhCountMask) return RT_E_ARG;   // leaf too large
+    // four-wide tree
+    if (b.nodes[0].left < 0) {
+        const int32_t r = leaf_ref(b.nodes[0]);
+        out.nodes4.emplace_back();
+        if (!make_node4(&b.nodes[0].box, &r, 1, out.nodes4[0])) return RT_E_ARG;
+        out.depth4 = 1;
+    } else {
+        Collapser c{b, out.nodes4};
+        c.run(0, 1);
+        if (!c.ok) return RT_E_ARG;   // a box no 8-bit grid can bound (coordinates near FLT_MAX)
+        out.depth4 = c.depth;
+    }
     if (b.nodes[0].left < 0) {   // the whole tree is one leaf: wrap it in a root with an empty sibling
         BvhNode root{};
         for (int k = 0; k < 3; ++k) {
@@ -268,6 +371,71 @@ int build_bvh(const HostScene &s, const std::vector<TriRec> &recs, HostBvh &out)
     }
     return RT_OK;
 }
+
+namespace {
+// The four-wide tree: decoded child boxes contain everything below them (nested boxes and padded
+// triangle boxes), every tree triangle in exactly one leaf, every node reached once, the stack
+// bound 3 * depth4 holds.
+int validate_bvh4(const HostScene &s, const std::vector<TriRec> &recs, const HostBvh &h, std::string &err) {
+    if (h.nodes4.empty()) { err = "no four-wide tree"; return RT_E_PARSE; }
+    std::vector<int> seen(recs.size(), 0);
+    std::vector<char> is_always(recs.size(), 0);
+    for (uint32_t t : h.always) is_always[t] = 1;
+    std::vector<int> node_seen(h.nodes4.size(), 0);
+    struct Item { int32_t ref; float lo[3], hi[3]; int depth; };
+    std::vector<Item> st{Item{0, {-FLT_MAX, -FLT_MAX, -FLT_MAX}, {FLT_MAX, FLT_MAX, FLT_MAX}, 0}};
+    while (!st.empty()) {
+        const Item it = st.back();
+        st.pop_back();
+        if (it.ref == kBvhEmpty) continue;
+        if (static_cast<uint32_t>(it.ref) & kBvhLeafBit) {
+            const uint32_t u = static_cast<uint32_t>(it.ref);
+            const uint32_t cnt = (u >> kBvhCountShift) & kBvhCountMask, first = u & ((1u << kBvhCountShift) - 1);
+            for (uint32_t i = first; i < first + cnt; ++i) {
+                const uint32_t t = h.leaf_tris[i];
+                seen[t]++;
+                float lo[3], hi[3];
+                bool never;
+                acceptance_box(recs[t], &s.verts[3 * s.tris[3 * t]], &s.verts[3 * s.tris[3 * t + 1]],
+                               &s.verts[3 * s.tris[3 * t + 2]], lo, hi, &never);
+                for (int k = 0; k < 3; ++k)
+                    if (lo[k] < it.lo[k] || hi[k] > it.hi[k]) { err = "4-wide: triangle box outside its leaf box"; return RT_E_PARSE; }
+            }
+            continue;
+        }
+        if (it.ref < 0 || static_cast<size_t>(it.ref) >= h.nodes4.size()) { err = "4-wide: bad node ref"; return RT_E_PARSE; }
+        if (node_seen[it.ref]++) { err = "4-wide: node reached twice"; return RT_E_PARSE; }
+        if (it.depth + 1 > h.depth4) { err = "4-wide: depth bound exceeded"; return RT_E_PARSE; }
+        const Bvh4Node &g = h.nodes4[it.ref];
+        for (int c = 0; c < 4; ++c) {
+            Item ch{g.child[c], {}, {}, it.depth + 1};
+            if (c >= g.n_children) {
+                if (g.child[c] != kBvhEmpty) { err = "4-wide: child past n_children"; return RT_E_PARSE; }
+                continue;
+            }
+            for (int k = 0; k < 3; ++k) {
+                ch.lo[k] = bvh4_decode(g.origin[k], g.ex[k], (g.qlo[k] >> (8 * c)) & 0xFF);
+                ch.hi[k] = bvh4_decode(g.origin[k], g.ex[k], (g.qhi[k] >> (8 * c)) & 0xFF);
+                if (ch.lo[k] < it.lo[k] || ch.hi[k] > it.hi[k]) {
+                    // a quantised child may stick out of its quantised parent; what matters is that
+                    // it contains its own content, checked below it. Clip for the nesting check.
+                    ch.lo[k] = std::max(ch.lo[k], it.lo[k]);
+                    ch.hi[k] = std::min(ch.hi[k], it.hi[k]);
+                }
+            }
+            st.push_back(ch);
+        }
+    }
+    for (size_t t = 0; t < recs.size(); ++t) {
+        const TriRec &T = recs[t];
+        const bool is_never = (T.n[0] == 0 && T.n[1] == 0 && T.n[2] == 0);
+        if (seen[t] != ((is_never || is_always[t]) ? 0 : 1)) { err = "4-wide: triangle not covered exactly once"; return RT_E_PARSE; }
+    }
+    for (int v : node_seen)
+        if (!v) { err = "4-wide: unreachable node"; return RT_E_PARSE; }
+    return RT_OK;
+}
+}  // namespace
 
 // Structural check used by tests: every tree triangle in exactly one leaf, every leaf's padded
 // triangle boxes inside its parent's stored child box, every node reachable, depth bound kept.
@@ -324,7 +492,7 @@ int validate_bvh(const HostScene &s, const std::vector<TriRec> &recs, const Host
     }
     if (inner_seen != h.nodes.size()) { err = "unreachable nodes"; return RT_E_PARSE; }
     if (never != h.n_never) { err = "degenerate count mismatch"; return RT_E_PARSE; }
-    return RT_OK;
+    return validate_bvh4(s, recs, h, err);
 }
 
 }  // namespace rt

@@ -73,8 +73,25 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 bytes");
 
+// Four children per node (64 B): child boxes quantised to 8 bits per bound in the node's frame.
+// Bound k of child c decodes as origin[k] + q * 2^ex[k] in float (the product is exact, so the
+// device's fmaf gives the same value); the builder picks q so the decoded box contains the child's
+// float box, so the exactness argument of the two-wide tree carries over unchanged.
+struct alignas(16) Bvh4Node {
+    float origin[3];
+    int8_t ex[3];
+    uint8_t n_children;
+    uint32_t qlo[3];      // byte c of qlo[k] = child c's lower bound on axis k
+    uint32_t qhi[3];
+    int32_t child[4];     // inner node index, leaf ref (kBvhLeafBit | count << 21 | first) or kBvhEmpty
+    uint32_t pad[2];
+};
+static_assert(sizeof(Bvh4Node) == 64, "Bvh4Node must be 64 bytes");
+
 struct HostBvh {
     std::vector<BvhNode> nodes;       // nodes[0] is the root
+    std::vector<Bvh4Node> nodes4;     // the same tree collapsed to four-wide nodes; nodes4[0] is the root
+    int depth4 = 0;                   // inner levels of the four-wide tree
     std::vector<uint32_t> leaf_tris;  // original triangle index of each leaf slot
     std::vector<uint32_t> always;     // ill-conditioned triangles every query tests
     size_t n_never = 0;               // n == 0: never accepted, never tested
@@ -85,6 +102,7 @@ struct HostBvh {
 bool acceptance_box(const TriRec &T, const float *v0, const float *v1, const float *v2, float lo[3], float hi[3],
                     bool *never);
 int build_bvh(const HostScene &s, const std::vector<TriRec> &recs, HostBvh &out);
+float bvh4_decode(float origin, int ex, uint32_t q);
 int validate_bvh(const HostScene &s, const std::vector<TriRec> &recs, const HostBvh &h, std::string &err);
 
 void build_tri_records(const HostScene &s, std::vector<TriRec> &out);

@@ -52,9 +52,14 @@ struct DevScene {
     int32_t use_bvh, n_always;
     float scene_m1;
     int32_t bvh_depth;              // traversal stack entries needed (tree depth)
+    const Bvh4Node *nodes4;         // the four-wide tree (bvh_width == 4)
+    int32_t bvh_width;              // 2 or 4 (RT_TUNE_BVH_WIDTH)
+    int32_t bvh4_stack;             // four-wide stack entries needed (3 per inner level)
+    int32_t lds_stack;              // stack entries per lane held in LDS (<= entries needed)
+    int32_t *stack_ovf;             // deeper entries: [entry - lds_stack][grid lane], grid <= bvh_grid
     int32_t xcd_split;              // RT_TUNE_XCD_SPLIT
     int32_t bvh_grid;               // RT_TUNE_BVH_GRID
-    unsigned long long *work;       // BVH kernels' triangle tests / node visits: [0..1] closest-hit, [2..3] shadow
+    unsigned long long *work;       // BVH kernels' work counters: [0, kWorkFields) closest-hit, then shadow
 };
 
 struct DevWork {
@@ -67,12 +72,16 @@ struct DevWork {
     float4 *chain_coef;             // [step][sample]: xyz = coefficient on the child's colour
     uint8_t *depth;                 // per sample: number of chain steps
     int32_t *counters;              // [step] main queue sizes (step 0 dense, incl. inactive), [kMaxStepsCounters + step] shadow
+    int32_t *wq;                    // [2 * step + shadow] work-queue slots of kWqSlot ints (RT_TUNE_XCD_SPLIT 2)
     int64_t cap;                    // samples per batch
     int32_t steps;                  // chain steps allocated (max_lvl + 1)
 };
 
 constexpr int kMaxStepsCounters = 4096;   // counters[step] for main queues; [kMaxStepsCounters + step] shadow
 constexpr int kErrorSlot = 2 * kMaxStepsCounters - 1;   // set by kernels on an internal inconsistency
+constexpr int kWorkFields = 6;               // = RT_WORK_FIELDS
+constexpr int kWqStride = 16;                // one 64-B line per segment counter
+constexpr int kWqSlot = 8 * kWqStride;       // eight segments (one per XCD) per launch
 
 // Launchers (all asynchronous on `stream`).
 void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream);

@@ -77,19 +77,6 @@ __device__ __forceinline__ float spec_powf(float x, float y) {
     return static_cast<float>(pow(static_cast<double>(x), static_cast<double>(y)));
 }
 
-// Wave-aggregated queue append: one atomic per wave, order within the wave preserved.
-__device__ __forceinline__ int wave_append(int32_t *counter, bool pred) {
-    const unsigned long long mask = __ballot(pred);
-    if (mask == 0) return -1;
-    const int lane = __lane_id();
-    const int leader = __ffsll(static_cast<long long>(mask)) - 1;
-    int base = 0;
-    if (lane == leader) base = atomicAdd(counter, __popcll(mask));
-    base = __shfl(base, leader);
-    const unsigned long long below = mask & ((1ull << lane) - 1ull);
-    return pred ? base + __popcll(below) : -1;
-}
-
 // Block-wide reservation in an output queue for kPer coalesced rounds of items: round k covers
 // items base + k*BLOCK + threadIdx.x, so reads and writes stay coalesced and the output keeps
 // input order. One atomicAdd per block chunk: a single counter word takes only ~88 atomics/us
@@ -203,6 +190,34 @@ constexpr int kBvhBlock = 128;
 
 struct RayBox { V3 o, inv; float pad, dlen; };
 
+// Per-lane traversal stack: the first `cap` entries in LDS ([entry][lane], conflict-free), deeper
+// entries in a global overflow area ([entry - cap][global lane], coalesced). Trees deeper than
+// the LDS part are rare, so a small LDS part keeps occupancy high at no cost in the common case.
+struct LaneStack {
+    int32_t (*lds)[kBvhBlock];
+    int32_t *ovf;
+    int cap, stride, gl;
+    __device__ __forceinline__ void push(int &sp, int32_t v) const {
+        if (sp < cap) lds[sp][threadIdx.x] = v;
+        else ovf[static_cast<size_t>(sp - cap) * stride + gl] = v;
+        ++sp;
+    }
+    __device__ __forceinline__ int32_t pop(int &sp) const {
+        --sp;
+        return sp < cap ? lds[sp][threadIdx.x] : ovf[static_cast<size_t>(sp - cap) * stride + gl];
+    }
+};
+
+__device__ __forceinline__ LaneStack lane_stack(const DevScene &sc, int32_t *lds) {
+    LaneStack st;
+    st.lds = reinterpret_cast<int32_t (*)[kBvhBlock]>(lds);
+    st.ovf = sc.stack_ovf;
+    st.cap = sc.lds_stack;
+    st.stride = static_cast<int>(gridDim.x) * kBvhBlock;
+    st.gl = static_cast<int>(blockIdx.x) * kBvhBlock + static_cast<int>(threadIdx.x);
+    return st;
+}
+
 __device__ __forceinline__ bool box_hit(const RayBox &R, float lx, float ly, float lz, float hx, float hy, float hz,
                                         float &tentry) {
     const float ax = (lx - R.pad - R.o.x) * R.inv.x, bx = (hx + R.pad - R.o.x) * R.inv.x;
@@ -216,7 +231,7 @@ __device__ __forceinline__ bool box_hit(const RayBox &R, float lx, float ly, flo
 
 template <bool kAnyHit>
 __device__ __forceinline__ void bvh_query(const DevScene &sc, V3 o, V3 dir, bool active, int &bidx, V3 &bI,
-                                          int32_t (*stack)[kBvhBlock], unsigned &tests, unsigned &visits) {
+                                          const LaneStack &stack, unsigned &tests, unsigned &visits) {
     float best = FLT_MAX;
     bool done = !active;
     // ill-conditioned triangles: every query, in index order (wave-uniform scalar loads)
@@ -231,7 +246,6 @@ __device__ __forceinline__ void bvh_query(const DevScene &sc, V3 o, V3 dir, bool
     R.inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
     R.pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
     R.dlen = sqrtf(dot(dir, dir));
-    const int lane = threadIdx.x;
     int sp = 0;
     int32_t ref = 0;
     while (true) {
@@ -249,7 +263,7 @@ __device__ __forceinline__ void bvh_query(const DevScene &sc, V3 o, V3 dir, bool
             const int32_t c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
             if (h0 && h1) {
                 const bool first0 = t0 <= t1;
-                stack[sp++][lane] = first0 ? c1 : c0;
+                stack.push(sp, first0 ? c1 : c0);
                 ref = first0 ? c0 : c1;
             } else if (h0) {
                 ref = c0;
@@ -257,7 +271,7 @@ __device__ __forceinline__ void bvh_query(const DevScene &sc, V3 o, V3 dir, bool
                 ref = c1;
             } else {
                 if (sp == 0) break;
-                ref = stack[--sp][lane];
+                ref = stack.pop(sp);
             }
         } else {
             const uint32_t u = static_cast<uint32_t>(ref);
@@ -270,9 +284,102 @@ __device__ __forceinline__ void bvh_query(const DevScene &sc, V3 o, V3 dir, bool
             tests += static_cast<unsigned>(cnt);
             if (kAnyHit && done) break;
             if (sp == 0) break;
-            ref = stack[--sp][lane];
+            ref = stack.pop(sp);
         }
     }
+}
+
+// Four-wide traversal over the quantised nodes (bvh.cpp, Bvh4Node). Same cull and leaf logic as
+// bvh_query; the hit children are sorted by entry distance, the nearest is visited next and the
+// others are pushed farthest first.
+__device__ __forceinline__ float q_decode(float origin, float scale, uint32_t word, int c) {
+    return fmaf(static_cast<float>((word >> (8 * c)) & 0xFFu), scale, origin);   // q * scale is exact
+}
+
+__device__ __forceinline__ void cswap(float &ta, int32_t &ra, float &tb, int32_t &rb) {
+    const bool sw = tb < ta;
+    const float t = sw ? tb : ta;
+    const int32_t r = sw ? rb : ra;
+    tb = sw ? ta : tb;
+    rb = sw ? ra : rb;
+    ta = t;
+    ra = r;
+}
+
+template <bool kAnyHit>
+__device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, bool active, int &bidx, V3 &bI,
+                                           const LaneStack &stack, unsigned &tests, unsigned &visits) {
+    float best = FLT_MAX;
+    bool done = !active;
+    for (int i = 0; i < sc.n_always; ++i) {
+        const int t = static_cast<int>(sc.always[i]);
+        const TriRec T = sc.tris[t];
+        test_triangle<kAnyHit, true>(T, t, o, dir, best, bidx, bI, done);
+    }
+    if (!active || (kAnyHit && done)) return;
+    RayBox R;
+    R.o = o;
+    R.inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+    R.pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
+    R.dlen = sqrtf(dot(dir, dir));
+    int sp = 0;
+    int32_t ref = 0;
+    while (true) {
+        if (ref >= 0) {
+            ++visits;
+            const uint4 *np = reinterpret_cast<const uint4 *>(sc.nodes4 + ref);
+            const uint4 a = np[0], b = np[1], c = np[2], d = np[3];
+            const float ox = __uint_as_float(a.x), oy = __uint_as_float(a.y), oz = __uint_as_float(a.z);
+            const float sx = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w)) + 127) << 23);
+            const float sy = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 8)) + 127) << 23);
+            const float sz = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 16)) + 127) << 23);
+            int32_t rc[4] = {static_cast<int32_t>(c.z), static_cast<int32_t>(c.w), static_cast<int32_t>(d.x),
+                             static_cast<int32_t>(d.y)};
+            float tc[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float te;
+                bool h = box_hit(R, q_decode(ox, sx, b.x, k), q_decode(oy, sy, b.y, k), q_decode(oz, sz, b.z, k),
+                                 q_decode(ox, sx, b.w, k), q_decode(oy, sy, c.x, k), q_decode(oz, sz, c.y, k), te);
+                h = h && rc[k] != kBvhEmpty;
+                if (!kAnyHit) h = h && (te * R.dlen - R.pad) * 0.99999f <= best;
+                tc[k] = h ? fminf(te, FLT_MAX) : INFINITY;   // hits sort before misses
+            }
+            cswap(tc[0], rc[0], tc[1], rc[1]);
+            cswap(tc[2], rc[2], tc[3], rc[3]);
+            cswap(tc[0], rc[0], tc[2], rc[2]);
+            cswap(tc[1], rc[1], tc[3], rc[3]);
+            cswap(tc[1], rc[1], tc[2], rc[2]);
+            if (tc[3] != INFINITY) stack.push(sp, rc[3]);
+            if (tc[2] != INFINITY) stack.push(sp, rc[2]);
+            if (tc[1] != INFINITY) stack.push(sp, rc[1]);
+            if (tc[0] != INFINITY) {
+                ref = rc[0];
+            } else {
+                if (sp == 0) break;
+                ref = stack.pop(sp);
+            }
+        } else {
+            const uint32_t u = static_cast<uint32_t>(ref);
+            const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
+            const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
+            for (int k = 0; k < cnt; ++k) {
+                const TriRec T = sc.leaf_recs[first + k];
+                test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first + k]), o, dir, best, bidx, bI, done);
+            }
+            tests += static_cast<unsigned>(cnt);
+            if (kAnyHit && done) break;
+            if (sp == 0) break;
+            ref = stack.pop(sp);
+        }
+    }
+}
+
+template <bool kAnyHit, int W>
+__device__ __forceinline__ void bvh_query_w(const DevScene &sc, V3 o, V3 dir, bool active, int &bidx, V3 &bI,
+                                            const LaneStack &stack, unsigned &tests, unsigned &visits) {
+    if (W == 4) bvh4_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
+    else bvh_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
 }
 
 // XCD-aware work split (cdna_hip_programming.md T1): blocks are dealt round-robin over the 8 XCDs,
@@ -280,6 +387,7 @@ __device__ __forceinline__ void bvh_query(const DevScene &sc, V3 o, V3 dir, bool
 // after their parents), so giving each XCD one contiguous eighth of the queue keeps the part of
 // the scene it touches small enough to stay in its 4 MB L2. Placement only changes speed.
 constexpr int kXcds = 8;
+constexpr int kWave = 64;
 struct Segment { int begin, end, step, start; };
 __device__ __forceinline__ Segment xcd_segment(int n, int block_dim, bool split) {
     const int nseg = split ? min(kXcds, static_cast<int>(gridDim.x)) : 1;   // every segment gets >= 1 block
@@ -295,31 +403,84 @@ __device__ __forceinline__ Segment xcd_segment(int n, int block_dim, bool split)
     return g;
 }
 
-// Wave-reduce two per-lane counters and add them to the scene's work counters.
-__device__ __forceinline__ void add_work(unsigned long long *work, unsigned tests, unsigned visits) {
-    unsigned long long a = tests, b = visits;
-    for (int off = 32; off > 0; off >>= 1) {
-        a += __shfl_xor(a, off);
-        b += __shfl_xor(b, off);
+// Per-kernel work counters (DevScene::work, kWorkFields per kind): ray-triangle tests, node
+// visits, the sum over wave tasks (64 queries side by side) of the largest per-lane visit count,
+// the largest visit count of any query, the number of wave tasks, the sum of per-task largest
+// test counts. visits / (64 * wave-max sum) is the SIMD efficiency of the traversal loop.
+struct WorkTally {
+    unsigned tests = 0, visits = 0, vmax = 0;
+    unsigned long long wave_vmax = 0, wave_tmax = 0, tasks = 0;
+    unsigned t0 = 0, v0 = 0;
+    __device__ __forceinline__ void begin() { t0 = tests; v0 = visits; }
+    __device__ __forceinline__ void end() {
+        unsigned dv = visits - v0, dt = tests - t0;
+        vmax = max(vmax, dv);
+        for (int off = 32; off > 0; off >>= 1) {
+            dv = max(dv, static_cast<unsigned>(__shfl_xor(static_cast<int>(dv), off)));
+            dt = max(dt, static_cast<unsigned>(__shfl_xor(static_cast<int>(dt), off)));
+        }
+        wave_vmax += dv;
+        wave_tmax += dt;
+        ++tasks;
     }
-    if (__lane_id() == 0 && work) {
-        atomicAdd(&work[0], a);
-        atomicAdd(&work[1], b);
+    __device__ __forceinline__ void flush(unsigned long long *work) {
+        if (!work) return;
+        unsigned long long a = tests, b = visits;
+        unsigned m = vmax;
+        for (int off = 32; off > 0; off >>= 1) {
+            a += __shfl_xor(a, off);
+            b += __shfl_xor(b, off);
+            m = max(m, static_cast<unsigned>(__shfl_xor(static_cast<int>(m), off)));
+        }
+        if (__lane_id() == 0) {
+            atomicAdd(&work[0], a);
+            atomicAdd(&work[1], b);
+            atomicAdd(&work[2], wave_vmax);
+            atomicMax(&work[3], static_cast<unsigned long long>(m));
+            atomicAdd(&work[4], tasks);
+            atomicAdd(&work[5], wave_tmax);
+        }
     }
+};
+
+// Query distribution for the BVH kernels. split 0: resident grid-stride over the queue. split 1:
+// each XCD's blocks stride over one contiguous eighth. split 2: the queue is cut into eight
+// segments with one counter each; a wave takes 64 queries at a time from its own XCD's segment
+// (screen-ordered, so the XCD's L2 holds a compact part of the scene) and, once that is empty,
+// from the others in turn, so no XCD idles while another has work. Every wave leaves after it has
+// seen all eight segments empty. Placement only changes speed, never results.
+template <typename F>
+__device__ __forceinline__ void drive_queries(int n, int split, int32_t *__restrict__ wq, F &&body) {
+    if (split == 2 && wq) {
+        const int lane = __lane_id();
+        const int home = blockIdx.x % kXcds;
+        const int chunk = (n + kXcds - 1) / kXcds;
+        for (int k = 0; k < kXcds;) {
+            const int g = (home + k) % kXcds;
+            const int begin = min(n, g * chunk), end = min(n, begin + chunk);
+            int base = 0;
+            if (lane == 0) base = atomicAdd(&wq[g * kWqStride], kWave);
+            base = begin + __shfl(base, 0);
+            if (base >= end) { ++k; continue; }
+            body(base + lane, end);
+        }
+        return;
+    }
+    const Segment seg = xcd_segment(n, kBvhBlock, split == 1);
+    for (int base = seg.start; base < seg.end; base += seg.step) body(base + static_cast<int>(threadIdx.x), seg.end);
 }
 
+template <int W>
 __global__ __launch_bounds__(kBvhBlock) void k_bvh_closest_hit(const DevScene sc, const float4 *__restrict__ q_org,
                                                                const float4 *__restrict__ q_dst,
                                                                const int32_t *__restrict__ q_count,
-                                                               int32_t *__restrict__ hit_idx, float4 *__restrict__ hit_I) {
+                                                               int32_t *__restrict__ hit_idx, float4 *__restrict__ hit_I,
+                                                               int32_t *__restrict__ wq) {
     extern __shared__ int32_t lds_stack[];
-    int32_t (*stack)[kBvhBlock] = reinterpret_cast<int32_t (*)[kBvhBlock]>(lds_stack);
-    const int n = *q_count;
-    unsigned tests = 0, visits = 0;
-    const Segment seg = xcd_segment(n, kBvhBlock, sc.xcd_split != 0);
-    for (int base = seg.start; base < seg.end; base += seg.step) {   // resident grid-stride within the XCD's segment
-        const int j = base + threadIdx.x;
-        bool active = j < seg.end;
+    const LaneStack stack = lane_stack(sc, lds_stack);
+    WorkTally wt;
+    drive_queries(*q_count, sc.xcd_split, wq, [&](int j, int end) {
+        bool active = j < end;
         V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
         if (active) {
             const float4 qo = q_org[j], qd = q_dst[j];
@@ -329,28 +490,27 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_closest_hit(const DevScene sc
         }
         int bidx = -1;
         V3 bI = mk(0, 0, 0);
-        bvh_query<false>(sc, o, dir, active, bidx, bI, stack, tests, visits);
-        if (j < seg.end) {
+        if (sc.work) wt.begin();
+        bvh_query_w<false, W>(sc, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
+        if (sc.work) wt.end();
+        if (j < end) {
             hit_idx[j] = bidx;
             hit_I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f);
         }
-    }
-    add_work(sc.work, tests, visits);
+    });
+    wt.flush(sc.work);
 }
 
-template <bool kAnyHit>
+template <bool kAnyHit, int W>
 __global__ __launch_bounds__(kBvhBlock) void k_bvh_shadow_hit(const DevScene sc, const float4 *__restrict__ q_org,
                                                               const float4 *__restrict__ q_dst,
                                                               const int32_t *__restrict__ q_count,
-                                                              uint8_t *__restrict__ shadow) {
+                                                              uint8_t *__restrict__ shadow, int32_t *__restrict__ wq) {
     extern __shared__ int32_t lds_stack[];
-    int32_t (*stack)[kBvhBlock] = reinterpret_cast<int32_t (*)[kBvhBlock]>(lds_stack);
-    const int n = *q_count;
-    unsigned tests = 0, visits = 0;
-    const Segment seg = xcd_segment(n, kBvhBlock, sc.xcd_split != 0);
-    for (int base = seg.start; base < seg.end; base += seg.step) {   // resident grid-stride within the XCD's segment
-        const int j = base + threadIdx.x;
-        const bool active = j < seg.end;
+    const LaneStack stack = lane_stack(sc, lds_stack);
+    WorkTally wt;
+    drive_queries(*q_count, sc.xcd_split, wq, [&](int j, int end) {
+        const bool active = j < end;
         V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
         int slot = 0;
         if (active) {
@@ -361,25 +521,27 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_shadow_hit(const DevScene sc,
         }
         int bidx = -1;
         V3 bI = mk(0, 0, 0);
-        bvh_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
+        if (sc.work) wt.begin();
+        bvh_query_w<kAnyHit, W>(sc, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
+        if (sc.work) wt.end();
         if (active) {
             uint8_t sh = 0;
             if (bidx >= 0) sh = sc.mats[sc.tri_mat[bidx]].transparent ? 0 : 1;
             shadow[slot] = sh;
         }
-    }
-    add_work(sc.work ? sc.work + 2 : nullptr, tests, visits);
+    });
+    wt.flush(sc.work ? sc.work + kWorkFields : nullptr);
 }
 
+template <int W>
 __global__ __launch_bounds__(kBvhBlock) void k_bvh_intersect_only(const DevScene sc, const float4 *__restrict__ q_org,
                                                                   const float4 *__restrict__ q_dst, int n,
                                                                   int32_t *__restrict__ idx, float4 *__restrict__ I) {
     extern __shared__ int32_t lds_stack[];
-    int32_t (*stack)[kBvhBlock] = reinterpret_cast<int32_t (*)[kBvhBlock]>(lds_stack);
-    unsigned tests = 0, visits = 0;
-    for (int base = blockIdx.x * kBvhBlock; base < n; base += gridDim.x * kBvhBlock) {
-        const int j = base + threadIdx.x;
-        const bool active = j < n;
+    const LaneStack stack = lane_stack(sc, lds_stack);
+    WorkTally wt;
+    drive_queries(n, 0, nullptr, [&](int j, int end) {
+        const bool active = j < end;
         V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
         if (active) {
             const float4 qo = q_org[j], qd = q_dst[j];
@@ -388,10 +550,12 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_intersect_only(const DevScene
         }
         int bidx = -1;
         V3 bI = mk(0, 0, 0);
-        bvh_query<false>(sc, o, dir, active, bidx, bI, stack, tests, visits);
+        if (sc.work) wt.begin();
+        bvh_query_w<false, W>(sc, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
+        if (sc.work) wt.end();
         if (active) { idx[j] = bidx; I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f); }
-    }
-    add_work(sc.work, tests, visits);
+    });
+    wt.flush(sc.work);
 }
 
 __global__ __launch_bounds__(kBlock) void k_closest_hit(const TriRec *__restrict__ tris, int nt,
@@ -812,8 +976,8 @@ void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevW
     hipLaunchKernelGGL(k_gen_rays, dim3(grid_for(n)), dim3(kBlock), 0, stream, org, dst, n, w);
 }
 
-// LDS stack bytes: one int per tree level per lane (the builder bounds the depth by kMaxBvhDepth)
-inline size_t bvh_lds(const DevScene &s) { return sizeof(int32_t) * kBvhBlock * static_cast<size_t>(s.bvh_depth); }
+// LDS part of the traversal stack: lds_stack entries per lane (the rest overflows to global)
+inline size_t bvh_lds(const DevScene &s) { return sizeof(int32_t) * kBvhBlock * static_cast<size_t>(std::max(s.lds_stack, 1)); }
 
 // 128-thread blocks with a 10-20 KB LDS stack: 16 resident per CU (32 waves) -> 4096 blocks.
 constexpr int kMaxBvhGrid = 4096;
@@ -830,8 +994,10 @@ inline unsigned grid_stride(int64_t n) {
 void launch_closest_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
     if (capacity <= 0) return;
     if (s.use_bvh) {
-        hipLaunchKernelGGL(k_bvh_closest_hit, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s,
-                           w.q_org[step & 1], w.q_dst[step & 1], &w.counters[step], w.hit_idx, w.hit_I);
+        auto k = s.bvh_width == 4 ? k_bvh_closest_hit<4> : k_bvh_closest_hit<2>;
+        hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s,
+                           w.q_org[step & 1], w.q_dst[step & 1], &w.counters[step], w.hit_idx, w.hit_I,
+                           w.wq + (2 * step) * kWqSlot);
         return;
     }
     hipLaunchKernelGGL(k_closest_hit, dim3(grid_for(capacity)), dim3(kBlock), 0, stream, s.tris, s.nt,
@@ -847,12 +1013,11 @@ void launch_shadow_gen(const DevScene &, const DevWork &w, const ShadeParams &p,
 void launch_shadow_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
     if (capacity <= 0) return;
     if (s.use_bvh) {
-        if (s.any_transparent)
-            hipLaunchKernelGGL(k_bvh_shadow_hit<false>, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s,
-                               w.sq_org, w.sq_dst, &w.counters[kMaxStepsCounters + step], w.shadow);
-        else
-            hipLaunchKernelGGL(k_bvh_shadow_hit<true>, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s,
-                               w.sq_org, w.sq_dst, &w.counters[kMaxStepsCounters + step], w.shadow);
+        auto k = s.bvh_width == 4 ? (s.any_transparent ? k_bvh_shadow_hit<false, 4> : k_bvh_shadow_hit<true, 4>)
+                                  : (s.any_transparent ? k_bvh_shadow_hit<false, 2> : k_bvh_shadow_hit<true, 2>);
+        hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s,
+                           w.sq_org, w.sq_dst, &w.counters[kMaxStepsCounters + step], w.shadow,
+                           w.wq + (2 * step + 1) * kWqSlot);
         return;
     }
     if (s.any_transparent)
@@ -884,7 +1049,8 @@ void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *d
                            float4 *I, hipStream_t stream) {
     if (n <= 0) return;
     if (s.use_bvh) {
-        hipLaunchKernelGGL(k_bvh_intersect_only, dim3(grid_bvh(n, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, org, dst, n, idx, I);
+        auto k = s.bvh_width == 4 ? k_bvh_intersect_only<4> : k_bvh_intersect_only<2>;
+        hipLaunchKernelGGL(k, dim3(grid_bvh(n, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, org, dst, n, idx, I);
         return;
     }
     hipLaunchKernelGGL(k_intersect_only, dim3(grid_for(n)), dim3(kBlock), 0, stream, s.tris, s.nt, org, dst, n, idx, I);

@@ -115,6 +115,7 @@ def test_bvh_structure(spec, workdir):
     nt = s.counts()[1]
     assert info["leaf_triangles"] + info["always"] + info["never"] == nt
     assert 1 <= info["depth"] <= 40
+    assert 1 <= info["depth4"] <= info["depth"] and 1 <= info["nodes4"] <= max(info["nodes"], 1)
     if nt > 1000:
         assert info["always"] < nt * 0.02   # dodgeColorTest: 184 slivers with < 1.6 degrees at T0
 
@@ -126,3 +127,31 @@ def test_bvh_on_tiny_and_degenerate_scenes(tmp_path):
     s.bvh_validate()
     info = s.bvh_info()
     assert info["never"] == 1 and info["leaf_triangles"] == 1
+
+
+def test_quantised_boxes_on_far_flat_and_tiny_geometry(tmp_path):
+    """Four-wide nodes store child boxes as 8-bit offsets on a power-of-two grid; bvh_validate
+    decodes every box exactly as the kernel does and checks it contains everything below it. This
+    scene mixes coordinates near 1e5 with features of 1e-3, exactly flat clusters (zero extent on
+    an axis) and a spread of scales, where the grid is coarsest relative to the children."""
+    rng = np.random.default_rng(3)
+    lines, nv = [], 0
+    for c in range(120):
+        base = rng.normal(size=3) * 10 ** rng.uniform(-2, 5)
+        scale = 10 ** rng.uniform(-3, 1)
+        flat = c % 4 == 0
+        for _ in range(6):
+            p0 = base + rng.normal(size=3) * scale
+            a, b = rng.normal(size=3) * scale, rng.normal(size=3) * scale
+            if flat:
+                p0[2] = base[2]; a[2] = 0; b[2] = 0
+            for v in (p0, p0 + a, p0 + b):
+                lines.append("v %.9g %.9g %.9g" % tuple(v))
+            lines.append("f %d %d %d" % (nv + 1, nv + 2, nv + 3))
+            nv += 3
+    p = tmp_path / "far.obj"
+    p.write_text("\n".join(lines) + "\n")
+    s = R.Scene.load(str(p), device=R.RT_HOST_ONLY)
+    s.bvh_validate()
+    info = s.bvh_info()
+    assert info["nodes4"] >= 1 and info["leaf_triangles"] + info["always"] + info["never"] == 720

@@ -192,8 +192,9 @@ def _query_mix(sc, rng, n):
     return o, d
 
 
+@pytest.mark.parametrize("width", [2, 4])
 @pytest.mark.parametrize("spec", ["ref:dodgeColorTest.obj", "ref:Models/shadow_test.obj", "syn:F4", "syn:C4"])
-def test_bvh_matches_brute_force_bitwise(spec, workdir, gpu_available):
+def test_bvh_matches_brute_force_bitwise(spec, width, workdir, gpu_available):
     path = scene_path(spec, workdir)
     rng = np.random.default_rng(17)
     with R.Scene.load(path, device=0) as sc:
@@ -201,6 +202,7 @@ def test_bvh_matches_brute_force_bitwise(spec, workdir, gpu_available):
         sc.set_accel("brute_force")
         bi, bp = sc.intersect_mesh(o, d)
         sc.set_accel("bvh")
+        sc.tune("bvh_width", width)
         assert sc.accel() == "bvh"
         vi, vp = sc.intersect_mesh(o, d)
     assert np.array_equal(bi, vi), np.nonzero(bi != vi)[0][:10]
@@ -213,13 +215,14 @@ def test_bvh_matches_brute_force_bitwise(spec, workdir, gpu_available):
         assert oi == bi[i] and np.array_equal(opt.view(np.uint32), bp[i].view(np.uint32))
 
 
-@pytest.mark.parametrize("accel", ["brute_force", "bvh"])
+@pytest.mark.parametrize("accel", ["brute_force", "bvh2", "bvh"])
 @pytest.mark.parametrize("name", ["F2b_shadow_test_160x120", "F3_spheres_128x72_pf2", "F4_refract_128x72"])
 def test_render_accel_modes_match_golden(name, accel, workdir, gpu_available):
     entry = golden_index()[name]
     gu8, gf32 = golden(name)
     with R.Scene.load(scene_path(entry["scene"], workdir), device=0) as sc:
-        sc.set_accel(accel)
+        sc.set_accel("bvh" if accel == "bvh2" else accel)
+        sc.tune("bvh_width", 2 if accel == "bvh2" else 4)
         u8, f32, counts = sc.render(_params(entry), want_f32=True)
     assert [int(c) for c in counts] == entry["counts"]
     _assert_image_close(u8, f32, gu8, gf32)
@@ -232,11 +235,14 @@ def test_c4_full_frame_bvh_equals_brute_force(workdir, gpu_available):
     with R.Scene.load(scene_path("syn:C4", workdir), device=0) as sc:
         sc.set_accel("bvh")
         a, af, ac = sc.render(p, want_f32=True)
+        sc.tune("bvh_width", 2)
+        a2, af2, ac2 = sc.render(p, want_f32=True)
         sc.set_accel("brute_force")
         b, bf, bc = sc.render(p, want_f32=True)
-    assert [int(x) for x in ac] == [int(x) for x in bc]
-    assert np.array_equal(a, b)
-    assert np.array_equal(af.view(np.uint32), bf.view(np.uint32))
+    for x, xf, xc in ((a, af, ac), (a2, af2, ac2)):
+        assert [int(v) for v in xc] == [int(v) for v in bc]
+        assert np.array_equal(x, b)
+        assert np.array_equal(xf.view(np.uint32), bf.view(np.uint32))
 
 
 def test_multi_frame_shard_batch_reassembles(workdir, gpu_available):
@@ -263,3 +269,21 @@ def test_multi_frame_shard_batch_reassembles(workdir, gpu_available):
     for f in frames:
         assert np.array_equal(f, full)
     assert [int(x) for x in total] == [3 * int(x) for x in counts]
+
+
+@pytest.mark.parametrize("knobs", [{"xcd_split": 0}, {"xcd_split": 1}, {"xcd_split": 2},
+                                   {"xcd_split": 2, "bvh_grid": 3}, {"xcd_split": 1, "bvh_grid": 5},
+                                   {"bvh_width": 2, "xcd_split": 2}, {"lds_stack": 1}, {"lds_stack": 5, "bvh_grid": 7},
+                                   {"bvh_width": 2, "lds_stack": 2}])
+def test_launch_shape_knobs_never_change_results(knobs, workdir, gpu_available):
+    """Query distribution (grid-stride, static XCD segments, work-stealing XCD queues), tiny grids
+    (fewer blocks than XCDs), tree width and the LDS/HBM split of the traversal stack (1 entry in
+    LDS: nearly every push overflows) are placement choices only: byte-identical frames."""
+    p = R.RenderParams(width=320, height=180, pf=2, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
+    with R.Scene.load(scene_path("syn:C4", workdir), device=0) as sc:
+        ref, reff, refc = sc.render(p, want_f32=True)
+        for k, v in knobs.items():
+            sc.tune(k, v)
+        u8, f32, c = sc.render(p, want_f32=True)
+    assert [int(x) for x in c] == [int(x) for x in refc]
+    assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))

@@ -24,6 +24,7 @@ sc = R.Scene.load(obj, device=0)
 p = R.RenderParams(width=1920, height=1080, pf=1, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
 ref, _, _ = sc.render(p)
 res = {i: [] for i in range(len(variants))}
+work = {}
 for r in range(rounds):
     for i, v in enumerate(variants):
         for k, val in v.items():
@@ -33,9 +34,19 @@ for r in range(rounds):
         u8, _, _ = sc.render(p)
         sc.set_profiling(False)
         assert np.array_equal(u8, ref), f"variant {v} changed the image"
+        q = {name: round(sc.kernel_stats(k)[2] / sc.counts()[1]) for name, k in
+             (("ch_queries", KERNEL_CLOSEST_HIT), ("shadow_queries", KERNEL_SHADOW))}
         res[i].append({name: sc.kernel_stats(k)[1] for name, k in
                        (("ch", KERNEL_CLOSEST_HIT), ("shadow", KERNEL_SHADOW), ("shade", KERNEL_SHADE), ("frame", KERNEL_FRAME))})
+        if r == 0:   # work counters slow the kernels: count once, untimed
+            sc.reset_stats()
+            sc.set_profiling(True, count_work=True)
+            sc.render(p)
+            sc.set_profiling(False)
+            work[i] = {name: sc.work_detail(k) for name, k in (("ch", KERNEL_CLOSEST_HIT), ("shadow", KERNEL_SHADOW))}
+            work[i].update(q)
 for i, v in enumerate(variants):
     med = {k: float(np.median([x[k] for x in res[i]])) for k in res[i][0]}
     tot = sum(med.values())
-    print(json.dumps({"variant": v, "median_ms": {k: round(x, 3) for k, x in med.items()}, "total_ms": round(tot, 3)}))
+    print(json.dumps({"variant": v, "median_ms": {k: round(x, 3) for k, x in med.items()}, "total_ms": round(tot, 3),
+                      "work_tests_visits": work[i]}))
