@@ -79,6 +79,7 @@ def parse():
     ap.add_argument("--accel", choices=("bvh", "brute_force"), default="bvh")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c4")
     ap.add_argument("--no-bf-roofline", action="store_true", help="skip the brute-force kernel's roofline frame")
+    ap.add_argument("--pipes", type=int, default=2, help="render pipelines a call's batches overlap on")
     return ap.parse_args()
 
 
@@ -116,6 +117,7 @@ def main():
     t_load = time.time()
     scene = R.Scene.load(obj, device=local_rank)
     scene.set_accel(args.accel)
+    scene.tune("pipes", args.pipes)
     t_load = time.time() - t_load
     bvh_info = scene.bvh_info() if args.accel == "bvh" else None
     nv, nt, nm = scene.counts()
@@ -173,6 +175,8 @@ def main():
 
     # ---- kernel timing for the roofline (HIP events on the scene's launch stream) ----
     def profile(steps):
+        # kernel durations in isolation: one pipeline, so no launch shares the GPU with another
+        scene.tune("pipes", 1)
         scene.reset_stats()
         scene.set_profiling(True)
         for _ in range(max(steps, 1)):
@@ -189,6 +193,7 @@ def main():
             torch.cuda.synchronize(dev)
             scene.set_profiling(False)
             work = scene.work_stats(KERNEL_CLOSEST_HIT)
+        scene.tune("pipes", args.pipes)
         return st, work
 
     stats, (bvh_tests, bvh_visits) = profile(args.profile_steps)

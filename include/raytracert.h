@@ -125,9 +125,11 @@ int rt_render_tile(rt_scene *scene, const rt_params *params, int32_t x0, int32_t
  * tile_w x tile_h tiles numbered row-major (tiles_x = ceil(width/tile_w), T tiles per frame); a batch
  * of `frames` frames of this view has tile ids g = f*T + t. This call renders ids first,
  * first+stride, first+2*stride, ... below frames*T and writes each as tile_w*tile_h*3 bytes (pixels
- * outside the frame are 0) into the DEVICE buffer d_out_u8 in that order. stream is a hipStream_t
- * (NULL = the scene's own stream); the call returns after enqueueing (no host synchronisation)
- * unless counts != NULL. Returns the number of tiles written via n_tiles_out. */
+ * outside the frame are 0) into the DEVICE buffer d_out_u8 in that order. stream is the caller's
+ * hipStream_t (NULL = the null stream): the work starts after what is already queued on it and
+ * later work queued on it sees the finished tiles (the renderer forks its pipelines from it and
+ * joins them back). The call returns after enqueueing (no host synchronisation) unless
+ * counts != NULL. Returns the number of tiles written via n_tiles_out. */
 int rt_render_tiles_device(rt_scene *scene, const rt_params *params, int32_t tile_w, int32_t tile_h,
                            int32_t frames, int32_t first, int32_t stride, void *d_out_u8, size_t out_capacity,
                            void *stream, int32_t *n_tiles_out, uint64_t counts[3]);
@@ -164,6 +166,7 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
 #define RT_TUNE_BVH_GRID  1   /* resident grid (blocks of 128 threads) of the BVH kernels */
 #define RT_TUNE_BVH_WIDTH 2   /* 4 (default): quantised four-wide nodes; 2: float binary nodes */
 #define RT_TUNE_LDS_STACK 3   /* traversal stack entries per lane kept in LDS; deeper ones in HBM */
+#define RT_TUNE_PIPES     4   /* 1-4 render pipelines (workspace + stream) a call's batches overlap on */
 int rt_scene_tune(rt_scene *scene, int32_t knob, int32_t value);
 
 /* ---- measurement ---------------------------------------------------------------------- */

@@ -212,10 +212,11 @@ class Scene:
                     leaf_triangles=int(info[4]), nodes4=int(info[5]), depth4=int(info[6]))
 
     def tune(self, knob: str, value: int) -> None:
-        """Launch-shape knobs ('xcd_split', 'bvh_grid', 'bvh_width', 'lds_stack'); outputs never
-        depend on them."""
+        """Launch-shape knobs ('xcd_split', 'bvh_grid', 'bvh_width', 'lds_stack', 'pipes');
+        outputs never depend on them."""
         k = {"xcd_split": _capi.TUNE_XCD_SPLIT, "bvh_grid": _capi.TUNE_BVH_GRID,
-             "bvh_width": _capi.TUNE_BVH_WIDTH, "lds_stack": _capi.TUNE_LDS_STACK}[knob]
+             "bvh_width": _capi.TUNE_BVH_WIDTH, "lds_stack": _capi.TUNE_LDS_STACK,
+             "pipes": _capi.TUNE_PIPES}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
 
     def bvh_validate(self) -> None:

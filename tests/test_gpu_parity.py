@@ -274,7 +274,8 @@ def test_multi_frame_shard_batch_reassembles(workdir, gpu_available):
 @pytest.mark.parametrize("knobs", [{"xcd_split": 0}, {"xcd_split": 1}, {"xcd_split": 2},
                                    {"xcd_split": 2, "bvh_grid": 3}, {"xcd_split": 1, "bvh_grid": 5},
                                    {"bvh_width": 2, "xcd_split": 2}, {"lds_stack": 1}, {"lds_stack": 5, "bvh_grid": 7},
-                                   {"bvh_width": 2, "lds_stack": 2}])
+                                   {"bvh_width": 2, "lds_stack": 2}, {"pipes": 1}, {"pipes": 3},
+                                   {"pipes": 4, "xcd_split": 2}])
 def test_launch_shape_knobs_never_change_results(knobs, workdir, gpu_available):
     """Query distribution (grid-stride, static XCD segments, work-stealing XCD queues), tiny grids
     (fewer blocks than XCDs), tree width and the LDS/HBM split of the traversal stack (1 entry in

@@ -23,12 +23,30 @@ obj = scenes.write_sphere_grid(spec, tempfile.mkdtemp(), "ab")
 sc = R.Scene.load(obj, device=0)
 p = R.RenderParams(width=1920, height=1080, pf=1, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
 ref, _, _ = sc.render(p)
+layout_tiles = ((p.width + 15) // 16) * ((p.height + 15) // 16)
+dbuf = torch.zeros(layout_tiles * 16 * 16 * 3, dtype=torch.uint8, device="cuda:0")
+cstream = torch.cuda.current_stream()
+cp = p.to_c()
+
+
+def wall_ms():
+    """One frame through rt_render_tiles_device on the caller's stream, profiling off."""
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(cstream)
+    sc.render_tiles_device(cp, 16, 16, 0, 1, dbuf.data_ptr(), dbuf.numel(), cstream.cuda_stream)
+    b.record(cstream)
+    b.synchronize()
+    return a.elapsed_time(b)
+
+
 res = {i: [] for i in range(len(variants))}
 work = {}
 for r in range(rounds):
     for i, v in enumerate(variants):
         for k, val in v.items():
             sc.tune(k, val)
+        wall_ms()
+        wall = wall_ms()
         sc.reset_stats()
         sc.set_profiling(True)
         u8, _, _ = sc.render(p)
@@ -38,6 +56,7 @@ for r in range(rounds):
              (("ch_queries", KERNEL_CLOSEST_HIT), ("shadow_queries", KERNEL_SHADOW))}
         res[i].append({name: sc.kernel_stats(k)[1] for name, k in
                        (("ch", KERNEL_CLOSEST_HIT), ("shadow", KERNEL_SHADOW), ("shade", KERNEL_SHADE), ("frame", KERNEL_FRAME))})
+        res[i][-1]["wall"] = wall
         if r == 0:   # work counters slow the kernels: count once, untimed
             sc.reset_stats()
             sc.set_profiling(True, count_work=True)
@@ -47,6 +66,6 @@ for r in range(rounds):
             work[i].update(q)
 for i, v in enumerate(variants):
     med = {k: float(np.median([x[k] for x in res[i]])) for k in res[i][0]}
-    tot = sum(med.values())
-    print(json.dumps({"variant": v, "median_ms": {k: round(x, 3) for k, x in med.items()}, "total_ms": round(tot, 3),
+    tot = sum(v_ for k_, v_ in med.items() if k_ != "wall")
+    print(json.dumps({"variant": v, "median_ms": {k: round(x, 3) for k, x in med.items()}, "kernel_sum_ms": round(tot, 3), "wall_ms": round(med["wall"], 3),
                       "work_tests_visits": work[i]}))
