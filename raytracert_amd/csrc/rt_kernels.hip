@@ -204,7 +204,11 @@ struct LaneStack {
     }
     __device__ __forceinline__ int32_t pop(int &sp) const {
         --sp;
-        return sp < cap ? lds[sp][threadIdx.x] : ovf[static_cast<size_t>(sp - cap) * stride + gl];
+        // the LDS read is unconditional so the two reads stay a ds_read and a global load (a
+        // select between the two pointers would become a slower flat load)
+        int32_t v = lds[min(sp, cap - 1)][threadIdx.x];
+        if (sp >= cap) v = ovf[static_cast<size_t>(sp - cap) * stride + gl];
+        return v;
     }
 };
 
@@ -227,6 +231,18 @@ __device__ __forceinline__ bool box_hit(const RayBox &R, float lx, float ly, flo
     const float tmax = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
     tentry = tmin;
     return tmin <= tmax * 1.00001f;
+}
+
+// A leaf's records in leaf order; the next record's load is issued before the current test so
+// one load is in flight behind the arithmetic. The original index (ties, result) is read only
+// when a test reaches the comparison with the current best.
+template <bool kAnyHit>
+__device__ __forceinline__ void test_leaf(const DevScene &sc, int first, int cnt, V3 o, V3 dir, float &best, int &bidx,
+                                          V3 &bI, bool &done) {
+    for (int k = 0; k < cnt; ++k) {
+        const TriRec T = sc.leaf_recs[first + k];
+        test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first + k]), o, dir, best, bidx, bI, done);
+    }
 }
 
 template <bool kAnyHit>
@@ -277,10 +293,7 @@ __device__ __forceinline__ void bvh_query(const DevScene &sc, V3 o, V3 dir, bool
             const uint32_t u = static_cast<uint32_t>(ref);
             const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
             const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
-            for (int k = 0; k < cnt; ++k) {
-                const TriRec T = sc.leaf_recs[first + k];
-                test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first + k]), o, dir, best, bidx, bI, done);
-            }
+            test_leaf<kAnyHit>(sc, first, cnt, o, dir, best, bidx, bI, done);
             tests += static_cast<unsigned>(cnt);
             if (kAnyHit && done) break;
             if (sp == 0) break;
@@ -363,10 +376,7 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
             const uint32_t u = static_cast<uint32_t>(ref);
             const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
             const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
-            for (int k = 0; k < cnt; ++k) {
-                const TriRec T = sc.leaf_recs[first + k];
-                test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first + k]), o, dir, best, bidx, bI, done);
-            }
+            test_leaf<kAnyHit>(sc, first, cnt, o, dir, best, bidx, bI, done);
             tests += static_cast<unsigned>(cnt);
             if (kAnyHit && done) break;
             if (sp == 0) break;
@@ -406,13 +416,16 @@ __device__ __forceinline__ Segment xcd_segment(int n, int block_dim, bool split)
 // Per-kernel work counters (DevScene::work, kWorkFields per kind): ray-triangle tests, node
 // visits, the sum over wave tasks (64 queries side by side) of the largest per-lane visit count,
 // the largest visit count of any query, the number of wave tasks, the sum of per-task largest
-// test counts. visits / (64 * wave-max sum) is the SIMD efficiency of the traversal loop.
+// test counts. visits / (64 * wave-max sum) is the SIMD efficiency of the traversal loop. Only
+// the kCount instantiations of the BVH kernels (RT_PROFILE_WORK) carry it.
+template <bool kOn>
 struct WorkTally {
     unsigned tests = 0, visits = 0, vmax = 0;
     unsigned long long wave_vmax = 0, wave_tmax = 0, tasks = 0;
     unsigned t0 = 0, v0 = 0;
-    __device__ __forceinline__ void begin() { t0 = tests; v0 = visits; }
+    __device__ __forceinline__ void begin() { if (kOn) { t0 = tests; v0 = visits; } }
     __device__ __forceinline__ void end() {
+        if (!kOn) return;
         unsigned dv = visits - v0, dt = tests - t0;
         vmax = max(vmax, dv);
         for (int off = 32; off > 0; off >>= 1) {
@@ -424,7 +437,7 @@ struct WorkTally {
         ++tasks;
     }
     __device__ __forceinline__ void flush(unsigned long long *work) {
-        if (!work) return;
+        if (!kOn || !work) return;
         unsigned long long a = tests, b = visits;
         unsigned m = vmax;
         for (int off = 32; off > 0; off >>= 1) {
@@ -449,28 +462,47 @@ struct WorkTally {
 // (screen-ordered, so the XCD's L2 holds a compact part of the scene) and, once that is empty,
 // from the others in turn, so no XCD idles while another has work. Every wave leaves after it has
 // seen all eight segments empty. Placement only changes speed, never results.
+struct QueryCursor {
+    int n, split, k = 0, base, step, end;
+    int32_t *wq;
+    __device__ __forceinline__ QueryCursor(int n_, int split_, int32_t *wq_) : n(n_), split(split_), wq(wq_) {
+        if (split == 2 && wq) return;
+        const Segment seg = xcd_segment(n, kBvhBlock, split == 1);
+        base = seg.start - seg.step;
+        step = seg.step;
+        end = seg.end;
+    }
+    // Next query index for this lane (may be >= end: inactive lane); false once the wave is done.
+    __device__ __forceinline__ bool next(int &j) {
+        if (split == 2 && wq) {
+            const int home = blockIdx.x % kXcds;
+            const int chunk = (n + kXcds - 1) / kXcds;
+            while (k < kXcds) {
+                const int g = (home + k) % kXcds;
+                const int begin = min(n, g * chunk);
+                end = min(n, begin + chunk);
+                int b = 0;
+                if (__lane_id() == 0) b = atomicAdd(&wq[g * kWqStride], kWave);
+                b = begin + __shfl(b, 0);
+                if (b < end) { j = b + __lane_id(); return true; }
+                ++k;
+            }
+            return false;
+        }
+        base += step;
+        j = base + static_cast<int>(threadIdx.x);
+        return base < end;
+    }
+};
+
 template <typename F>
 __device__ __forceinline__ void drive_queries(int n, int split, int32_t *__restrict__ wq, F &&body) {
-    if (split == 2 && wq) {
-        const int lane = __lane_id();
-        const int home = blockIdx.x % kXcds;
-        const int chunk = (n + kXcds - 1) / kXcds;
-        for (int k = 0; k < kXcds;) {
-            const int g = (home + k) % kXcds;
-            const int begin = min(n, g * chunk), end = min(n, begin + chunk);
-            int base = 0;
-            if (lane == 0) base = atomicAdd(&wq[g * kWqStride], kWave);
-            base = begin + __shfl(base, 0);
-            if (base >= end) { ++k; continue; }
-            body(base + lane, end);
-        }
-        return;
-    }
-    const Segment seg = xcd_segment(n, kBvhBlock, split == 1);
-    for (int base = seg.start; base < seg.end; base += seg.step) body(base + static_cast<int>(threadIdx.x), seg.end);
+    QueryCursor c(n, split, wq);
+    int j;
+    while (c.next(j)) body(j, c.end);
 }
 
-template <int W>
+template <int W, bool kCount>
 __global__ __launch_bounds__(kBvhBlock) void k_bvh_closest_hit(const DevScene sc, const float4 *__restrict__ q_org,
                                                                const float4 *__restrict__ q_dst,
                                                                const int32_t *__restrict__ q_count,
@@ -478,7 +510,7 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_closest_hit(const DevScene sc
                                                                int32_t *__restrict__ wq) {
     extern __shared__ int32_t lds_stack[];
     const LaneStack stack = lane_stack(sc, lds_stack);
-    WorkTally wt;
+    WorkTally<kCount> wt;
     drive_queries(*q_count, sc.xcd_split, wq, [&](int j, int end) {
         bool active = j < end;
         V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
@@ -490,9 +522,9 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_closest_hit(const DevScene sc
         }
         int bidx = -1;
         V3 bI = mk(0, 0, 0);
-        if (sc.work) wt.begin();
+        wt.begin();
         bvh_query_w<false, W>(sc, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
-        if (sc.work) wt.end();
+        wt.end();
         if (j < end) {
             hit_idx[j] = bidx;
             hit_I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f);
@@ -501,14 +533,14 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_closest_hit(const DevScene sc
     wt.flush(sc.work);
 }
 
-template <bool kAnyHit, int W>
+template <bool kAnyHit, int W, bool kCount>
 __global__ __launch_bounds__(kBvhBlock) void k_bvh_shadow_hit(const DevScene sc, const float4 *__restrict__ q_org,
                                                               const float4 *__restrict__ q_dst,
                                                               const int32_t *__restrict__ q_count,
                                                               uint8_t *__restrict__ shadow, int32_t *__restrict__ wq) {
     extern __shared__ int32_t lds_stack[];
     const LaneStack stack = lane_stack(sc, lds_stack);
-    WorkTally wt;
+    WorkTally<kCount> wt;
     drive_queries(*q_count, sc.xcd_split, wq, [&](int j, int end) {
         const bool active = j < end;
         V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
@@ -521,9 +553,9 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_shadow_hit(const DevScene sc,
         }
         int bidx = -1;
         V3 bI = mk(0, 0, 0);
-        if (sc.work) wt.begin();
+        wt.begin();
         bvh_query_w<kAnyHit, W>(sc, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
-        if (sc.work) wt.end();
+        wt.end();
         if (active) {
             uint8_t sh = 0;
             if (bidx >= 0) sh = sc.mats[sc.tri_mat[bidx]].transparent ? 0 : 1;
@@ -533,13 +565,13 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_shadow_hit(const DevScene sc,
     wt.flush(sc.work ? sc.work + kWorkFields : nullptr);
 }
 
-template <int W>
+template <int W, bool kCount>
 __global__ __launch_bounds__(kBvhBlock) void k_bvh_intersect_only(const DevScene sc, const float4 *__restrict__ q_org,
                                                                   const float4 *__restrict__ q_dst, int n,
                                                                   int32_t *__restrict__ idx, float4 *__restrict__ I) {
     extern __shared__ int32_t lds_stack[];
     const LaneStack stack = lane_stack(sc, lds_stack);
-    WorkTally wt;
+    WorkTally<kCount> wt;
     drive_queries(n, 0, nullptr, [&](int j, int end) {
         const bool active = j < end;
         V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
@@ -550,9 +582,9 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_intersect_only(const DevScene
         }
         int bidx = -1;
         V3 bI = mk(0, 0, 0);
-        if (sc.work) wt.begin();
+        wt.begin();
         bvh_query_w<false, W>(sc, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
-        if (sc.work) wt.end();
+        wt.end();
         if (active) { idx[j] = bidx; I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f); }
     });
     wt.flush(sc.work);
@@ -994,7 +1026,8 @@ inline unsigned grid_stride(int64_t n) {
 void launch_closest_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
     if (capacity <= 0) return;
     if (s.use_bvh) {
-        auto k = s.bvh_width == 4 ? k_bvh_closest_hit<4> : k_bvh_closest_hit<2>;
+        auto k = s.work ? (s.bvh_width == 4 ? k_bvh_closest_hit<4, true> : k_bvh_closest_hit<2, true>)
+                        : (s.bvh_width == 4 ? k_bvh_closest_hit<4, false> : k_bvh_closest_hit<2, false>);
         hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s,
                            w.q_org[step & 1], w.q_dst[step & 1], &w.counters[step], w.hit_idx, w.hit_I,
                            w.wq + (2 * step) * kWqSlot);
@@ -1013,8 +1046,11 @@ void launch_shadow_gen(const DevScene &, const DevWork &w, const ShadeParams &p,
 void launch_shadow_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
     if (capacity <= 0) return;
     if (s.use_bvh) {
-        auto k = s.bvh_width == 4 ? (s.any_transparent ? k_bvh_shadow_hit<false, 4> : k_bvh_shadow_hit<true, 4>)
-                                  : (s.any_transparent ? k_bvh_shadow_hit<false, 2> : k_bvh_shadow_hit<true, 2>);
+        auto k = s.bvh_width == 4 ? (s.any_transparent ? k_bvh_shadow_hit<false, 4, false> : k_bvh_shadow_hit<true, 4, false>)
+                                  : (s.any_transparent ? k_bvh_shadow_hit<false, 2, false> : k_bvh_shadow_hit<true, 2, false>);
+        if (s.work)
+            k = s.bvh_width == 4 ? (s.any_transparent ? k_bvh_shadow_hit<false, 4, true> : k_bvh_shadow_hit<true, 4, true>)
+                                 : (s.any_transparent ? k_bvh_shadow_hit<false, 2, true> : k_bvh_shadow_hit<true, 2, true>);
         hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s,
                            w.sq_org, w.sq_dst, &w.counters[kMaxStepsCounters + step], w.shadow,
                            w.wq + (2 * step + 1) * kWqSlot);
@@ -1049,7 +1085,8 @@ void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *d
                            float4 *I, hipStream_t stream) {
     if (n <= 0) return;
     if (s.use_bvh) {
-        auto k = s.bvh_width == 4 ? k_bvh_intersect_only<4> : k_bvh_intersect_only<2>;
+        auto k = s.work ? (s.bvh_width == 4 ? k_bvh_intersect_only<4, true> : k_bvh_intersect_only<2, true>)
+                        : (s.bvh_width == 4 ? k_bvh_intersect_only<4, false> : k_bvh_intersect_only<2, false>);
         hipLaunchKernelGGL(k, dim3(grid_bvh(n, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, org, dst, n, idx, I);
         return;
     }
