@@ -10,7 +10,8 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librtamd.so")
+# RTAMD_LIB selects another in-tree build of the same library (A/B of kernel variants, tools/)
+LIB_PATH = os.environ.get("RTAMD_LIB") or os.path.join(HERE, "librtamd.so")
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "raytracert.h")
 
 RT_OK = 0

@@ -305,8 +305,8 @@ __device__ __forceinline__ void bvh_query(const DevScene &sc, V3 o, V3 dir, bool
 // Four-wide traversal over the quantised nodes (bvh.cpp, Bvh4Node). Same cull and leaf logic as
 // bvh_query; the hit children are sorted by entry distance, the nearest is visited next and the
 // others are pushed farthest first.
-__device__ __forceinline__ float q_decode(float origin, float scale, uint32_t word, int c) {
-    return fmaf(static_cast<float>((word >> (8 * c)) & 0xFFu), scale, origin);   // q * scale is exact
+__device__ __forceinline__ float q_decode(float base, float scale, uint32_t word, int c) {
+    return fmaf(static_cast<float>((word >> (8 * c)) & 0xFFu), scale, base);   // q * scale is exact
 }
 
 __device__ __forceinline__ void cswap(float &ta, int32_t &ra, float &tb, int32_t &rb) {
@@ -348,12 +348,20 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
             const float sz = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 16)) + 127) << 23);
             int32_t rc[4] = {static_cast<int32_t>(c.z), static_cast<int32_t>(c.w), static_cast<int32_t>(d.x),
                              static_cast<int32_t>(d.y)};
+            // The ray origin and pad are folded into the node frame once: a bound's slab distance is
+            // fma(q, scale, origin -/+ pad - o) * inv, the same rounding budget as box_hit's
+            // (bound - pad - o) * inv (bvh.cpp: both are far inside the pad's margin).
+            const float lx = (ox - R.pad) - R.o.x, ly = (oy - R.pad) - R.o.y, lz = (oz - R.pad) - R.o.z;
+            const float hx = (ox + R.pad) - R.o.x, hy = (oy + R.pad) - R.o.y, hz = (oz + R.pad) - R.o.z;
             float tc[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                float te;
-                bool h = box_hit(R, q_decode(ox, sx, b.x, k), q_decode(oy, sy, b.y, k), q_decode(oz, sz, b.z, k),
-                                 q_decode(ox, sx, b.w, k), q_decode(oy, sy, c.x, k), q_decode(oz, sz, c.y, k), te);
+                const float ax = q_decode(lx, sx, b.x, k) * R.inv.x, bx = q_decode(hx, sx, b.w, k) * R.inv.x;
+                const float ay = q_decode(ly, sy, b.y, k) * R.inv.y, by = q_decode(hy, sy, c.x, k) * R.inv.y;
+                const float az = q_decode(lz, sz, b.z, k) * R.inv.z, bz = q_decode(hz, sz, c.y, k) * R.inv.z;
+                const float te = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
+                const float tx = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                bool h = te <= tx * 1.00001f;
                 h = h && rc[k] != kBvhEmpty;
                 if (!kAnyHit) h = h && (te * R.dlen - R.pad) * 0.99999f <= best;
                 tc[k] = h ? fminf(te, FLT_MAX) : INFINITY;   // hits sort before misses
