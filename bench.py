@@ -126,23 +126,39 @@ def main():
 
     layout = rdist.TileLayout(WIDTH, HEIGHT, TILE, TILE)
     plan = rdist.ShardPlan(layout, world, frames=world if args.mode == "weak" else 1)
-    buf = torch.zeros(plan.shard_bytes, dtype=torch.uint8, device=dev)
+    # two shard buffers: step i renders into bufs[i % 2] while step i-1's gather reads the other
+    bufs = [torch.zeros(plan.shard_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
     index = torch.as_tensor(plan.gather_index(), device=dev)
     stream = torch.cuda.current_stream(dev)
 
-    def render_shard(want_counts=False):
+    def render_shard(want_counts=False, buf=None):
         # one call: this rank's tile ids rank, rank + N, ... over the step's `frames` frames
+        buf = bufs[0] if buf is None else buf
         n, c = scene.render_tiles_device(cparams, TILE, TILE, rank, world, buf.data_ptr(), buf.numel(),
                                          stream.cuda_stream, want_counts=want_counts, frames=plan.frames)
         assert n == plan.rank_tiles(rank)
         return c if c is not None else np.zeros(3, np.uint64)
 
-    def step():
-        render_shard()
-        gathered = rdist.gather_shards(buf, rank, world)
-        if rank == 0:
-            return rdist.assemble_plan_torch(gathered, plan, index)
-        return None
+    pending = []
+
+    def finish(p):
+        # order the stream after the gather, then un-permute on rank 0
+        if p is None:
+            return None
+        gathered, work = p
+        if work is not None:
+            work.wait()
+        return rdist.assemble_plan_torch(gathered, plan, index) if rank == 0 else None
+
+    def step(i):
+        """Render step i's shard, start its gather (async, on the collective's stream) and finish
+        step i-1's: the gather of one step overlaps the next step's render."""
+        render_shard(buf=bufs[i % 2])
+        pending.append(rdist.gather_shards(bufs[i % 2], rank, world, async_op=True))
+        return finish(pending.pop(0)) if len(pending) > 1 else None
+
+    def drain():
+        return finish(pending.pop(0)) if pending else None
 
     # rays per step (deterministic): counted once, summed over ranks
     counts = render_shard(want_counts=True)
@@ -152,8 +168,9 @@ def main():
     rays_per_step = float(ct.sum().item())
     rays_by_kind = [int(x) for x in ct.tolist()]
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        step(i)
+    drain()
     torch.cuda.synchronize(dev)
 
     # ---- timed region ----
@@ -162,8 +179,11 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     frames = None
-    for _ in range(args.steps):
-        frames = step()
+    for i in range(args.steps):
+        f = step(i)
+        frames = f if f is not None else frames
+    f = drain()   # the last step's gather + un-permute stay inside the timed region
+    frames = f if f is not None else frames
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

@@ -93,19 +93,19 @@ def assemble_torch(gathered, layout: TileLayout, world: int, index=None):
     return frame[: layout.height, : layout.width]
 
 
-def gather_shards(buf, rank: int, world: int, group=None):
+def gather_shards(buf, rank: int, world: int, group=None, async_op: bool = False):
     """One collective: gather every rank's equal-sized shard buffer to rank 0. Returns the
-    concatenated tensor on rank 0 (None elsewhere). world == 1 returns buf itself."""
+    concatenated tensor on rank 0 (None elsewhere); world == 1 returns buf itself. With async_op
+    it returns (tensor, work): the gather runs on the collective's own stream and work.wait()
+    orders the caller's stream after it, so the next shard can render meanwhile (into another
+    buffer)."""
     import torch
     import torch.distributed as dist
     if world == 1:
-        return buf
-    if rank == 0:
-        out = torch.empty(world * buf.numel(), dtype=buf.dtype, device=buf.device)
-        dist.gather(buf, list(out.chunk(world)), dst=0, group=group)
-        return out
-    dist.gather(buf, None, dst=0, group=group)
-    return None
+        return (buf, None) if async_op else buf
+    out = torch.empty(world * buf.numel(), dtype=buf.dtype, device=buf.device) if rank == 0 else None
+    work = dist.gather(buf, list(out.chunk(world)) if rank == 0 else None, dst=0, group=group, async_op=async_op)
+    return (out, work) if async_op else out
 
 
 def render_frame_sharded(render_shard, layout: TileLayout, rank: int, world: int, buf, group=None, index=None):

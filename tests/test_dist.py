@@ -34,7 +34,7 @@ def stub_render(layout, first, stride):
     return np.stack(tiles) if tiles else np.zeros((0, layout.tile_h, layout.tile_w, 3), np.uint8)
 
 
-def _worker(rank, world, port, mode, result_path):
+def _worker(rank, world, port, mode, result_path, async_op=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     layout = rdist.TileLayout(100, 70, 16, 16)
@@ -46,7 +46,11 @@ def _worker(rank, world, port, mode, result_path):
         buf[off:off + t.size] = torch.from_numpy(t)
         off += t.size
     assert off == plan.rank_tiles(rank) * layout.tile_bytes
-    gathered = rdist.gather_shards(buf, rank, world)
+    if async_op:   # bench.py's pipelined form: the gather's work handle is waited on later
+        gathered, work = rdist.gather_shards(buf, rank, world, async_op=True)
+        work.wait()
+    else:
+        gathered = rdist.gather_shards(buf, rank, world)
     if rank == 0:
         frames = rdist.assemble_plan_torch(gathered, plan).numpy()
         np.save(result_path, frames, allow_pickle=False)
@@ -62,10 +66,11 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,mode", [(2, "weak"), (2, "strong"), (3, "weak"), (3, "strong")])
-def test_gloo_shard_gather_assemble(tmp_path, world, mode):
+@pytest.mark.parametrize("world,mode,async_op", [(2, "weak", False), (2, "strong", False), (3, "weak", False),
+                                                 (3, "strong", False), (2, "weak", True), (3, "weak", True)])
+def test_gloo_shard_gather_assemble(tmp_path, world, mode, async_op):
     out = str(tmp_path / "frames.npy")
-    mp.spawn(_worker, args=(world, _free_port(), mode, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), mode, out, async_op), nprocs=world, join=True)
     frames = np.load(out, allow_pickle=False)
     expect = pattern(100, 70)
     assert frames.shape == ((world if mode == "weak" else 1), 70, 100, 3)
