@@ -97,6 +97,13 @@ int rt_device_count(int32_t *count);
 
 /* ---- scene ---------------------------------------------------------------------------- */
 int  rt_scene_load_obj(const char *path, int32_t device, rt_scene **out);
+/* load_flags: RT_LOAD_PARALLEL (what rt_scene_load_obj does: the file is parsed by up to 16
+ * threads) or RT_LOAD_SEQUENTIAL (one fgets/sscanf pass, the reference loader restated line by
+ * line). Both produce the same vertices, triangles, materials and normals bit for bit. */
+#define RT_LOAD_PARALLEL   0
+#define RT_LOAD_SEQUENTIAL 1
+#define RT_LOAD_THREADS(n) ((n) << 8)   /* with RT_LOAD_PARALLEL: exactly n parser threads (tests) */
+int  rt_scene_load_obj_ex(const char *path, int32_t device, int32_t load_flags, rt_scene **out);
 int  rt_scene_create(const float *xyz, int32_t n_vertices, const uint32_t *tri_v, const uint32_t *tri_mat,
                      int32_t n_triangles, const rt_material *materials, int32_t n_materials,
                      int32_t device, rt_scene **out);

@@ -33,6 +33,7 @@ KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME = range(4)
 ACCEL_BRUTE_FORCE, ACCEL_BVH = 0, 1
 TUNE_XCD_SPLIT, TUNE_BVH_GRID, TUNE_BVH_WIDTH, TUNE_LDS_STACK, TUNE_PIPES = 0, 1, 2, 3, 4
 BVH_INFO_FIELDS = 7
+LOAD_PARALLEL, LOAD_SEQUENTIAL = 0, 1
 WORK_FIELDS = 6
 
 
@@ -67,6 +68,7 @@ _SIGNATURES = {
     "rt_last_error_string": ([], C.c_char_p),
     "rt_device_count": ([C.POINTER(C.c_int32)], C.c_int),
     "rt_scene_load_obj": ([C.c_char_p, C.c_int32, C.POINTER(_VP)], C.c_int),
+    "rt_scene_load_obj_ex": ([C.c_char_p, C.c_int32, C.c_int32, C.POINTER(_VP)], C.c_int),
     "rt_scene_create": ([_VP, C.c_int32, _VP, _VP, C.c_int32, _VP, C.c_int32, C.c_int32, C.POINTER(_VP)], C.c_int),
     "rt_scene_destroy": ([_VP], None),
     "rt_scene_info": ([_VP, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)], C.c_int),

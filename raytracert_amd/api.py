@@ -78,10 +78,13 @@ class Scene:
 
     # -- construction ------------------------------------------------------------------------
     @classmethod
-    def load(cls, path: str, device: int = 0) -> "Scene":
-        """init(fileName): Mesh::loadMesh + loadMtl + calculateNormals."""
+    def load(cls, path: str, device: int = 0, sequential: bool = False, threads: int = 0) -> "Scene":
+        """init(fileName): Mesh::loadMesh + loadMtl + calculateNormals. The default parser is
+        parallel (threads=0: automatic); sequential=True runs the line-by-line restatement (same
+        result)."""
         h = C.c_void_p()
-        check(lib().rt_scene_load_obj(path.encode(), device, C.byref(h)))
+        flags = _capi.LOAD_SEQUENTIAL if sequential else (_capi.LOAD_PARALLEL | (int(threads) << 8))
+        check(lib().rt_scene_load_obj_ex(path.encode(), device, flags, C.byref(h)))
         return cls(h, device)
 
     @classmethod

@@ -105,6 +105,27 @@ int build_bvh(const HostScene &s, const std::vector<TriRec> &recs, HostBvh &out)
 float bvh4_decode(float origin, int ex, uint32_t q);
 int validate_bvh(const HostScene &s, const std::vector<TriRec> &recs, const HostBvh &h, std::string &err);
 
+// OBJ reader material state shared by the sequential and the parallel parser (scene_loader.cpp).
+struct MtlIndex;
+class ObjControlState {
+  public:
+    ObjControlState(const char *path, HostScene &s);
+    ~ObjControlState();
+    ObjControlState(const ObjControlState &) = delete;
+    ObjControlState &operator=(const ObjControlState &) = delete;
+    void mtllib(char *line);    // an "mtllib ..." chunk
+    void usemtl(char *line);    // a "usemtl ..." chunk
+    int current_material() const;
+
+  private:
+    HostScene &s;
+    MtlIndex *index;
+    std::string prefix, matname;
+};
+void finish_obj(HostScene &s);
+// Parallel parser, same result as load_obj (obj_parallel.cpp); threads <= 0: up to 16.
+int load_obj_parallel(const char *path, HostScene &s, std::string &err, int threads);
+
 void build_tri_records(const HostScene &s, std::vector<TriRec> &out);
 void build_dev_materials(const HostScene &s, std::vector<DevMaterial> &out);
 

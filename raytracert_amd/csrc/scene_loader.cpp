@@ -26,11 +26,6 @@
 #include "rt_internal.h"
 
 namespace rt {
-namespace {
-
-constexpr int kLineLen = 256;   // mesh.cpp:22
-
-constexpr uint32_t kValidMask = RT_HAS_KD | RT_HAS_KA | RT_HAS_KS | RT_HAS_TR;  // is_valid(), mesh.h:55-56
 
 struct MtlIndex {
     std::unordered_map<std::string, int> by_name;   // std::map<string,uint> materialIndex
@@ -39,6 +34,13 @@ struct MtlIndex {
         return it == by_name.end() ? -1 : it->second;
     }
 };
+
+namespace {
+
+constexpr int kLineLen = 256;   // mesh.cpp:22
+
+constexpr uint32_t kValidMask = RT_HAS_KD | RT_HAS_KA | RT_HAS_KS | RT_HAS_TR;  // is_valid(), mesh.h:55-56
+
 
 // Mesh::loadMtl, mesh.cpp:334-460
 void load_mtl(const std::string &filename, HostScene &s, MtlIndex &index) {
@@ -108,15 +110,10 @@ void load_mtl(const std::string &filename, HostScene &s, MtlIndex &index) {
 
 }  // namespace
 
-int load_obj(const char *path, HostScene &s, std::string &err) {
-    s = HostScene();
-    FILE *in = std::fopen(path, "r");
-    if (!in) {
-        err = std::string("cannot open OBJ file '") + path + "'";
-        return RT_E_IO;
-    }
-    // defaultMat, mesh.cpp:108-117
-    HostMaterial def;
+// The OBJ reader's material state (mesh.cpp:108-117 default material, :157-178 mtllib, :180-193
+// usemtl), shared by the sequential and the parallel parser so both replay it identically.
+ObjControlState::ObjControlState(const char *path, HostScene &scene) : s(scene), index(new MtlIndex) {
+    HostMaterial def;   // defaultMat, mesh.cpp:108-117
     def.Kd[0] = def.Kd[1] = def.Kd[2] = 0.5f;
     def.Ks[0] = def.Ks[1] = def.Ks[2] = 0.5f;
     def.Ns = 96.7f;
@@ -124,16 +121,66 @@ int load_obj(const char *path, HostScene &s, std::string &err) {
     def.flags = RT_HAS_KD | RT_HAS_KA | RT_HAS_KS | RT_HAS_NS | RT_HAS_ILLUM;
     def.name = "StandardMaterialInitFromTriMesh";
     s.mats.push_back(def);
-    MtlIndex index;
-
     std::string real(path);
     for (char &c : real) if (c == '\\') c = '/';
-    std::string prefix;
-    size_t slash = real.rfind('/');
+    const size_t slash = real.rfind('/');
     if (slash != std::string::npos) prefix = real.substr(0, slash + 1);
+}
 
+ObjControlState::~ObjControlState() { delete index; }
+
+void ObjControlState::mtllib(char *line) {
+    char *p0 = line + 6;
+    while (std::isspace(static_cast<unsigned char>(*++p0))) {}
+    size_t i = 0;
+    while (p0[i] && !(static_cast<signed char>(p0[i]) < 32)) ++i;
+    prefix.append(p0, i);      // path_.append(...) mutates the prefix (mesh.cpp:173-175)
+    load_mtl(prefix, s, *index);
+}
+
+void ObjControlState::usemtl(char *line) {
+    char *p0 = line + 6;
+    while (std::isspace(static_cast<unsigned char>(*++p0))) {}
+    char *p1 = p0;
+    while (*p1 && !std::isspace(static_cast<unsigned char>(*p1))) ++p1;
+    matname.assign(p0, p1);
+    if (index->find(matname) < 0) {
+        std::fprintf(stderr, "Warning! Material '%s' not defined in material file. Taking default!\n", matname.c_str());
+        matname.clear();
+    }
+}
+
+int ObjControlState::current_material() const {
+    const int m = matname.empty() ? -1 : index->find(matname);
+    return m < 0 ? 0 : m;
+}
+
+// Drop triangles referencing non-existent vertices (reference: out-of-bounds read), then the
+// face normals.
+void finish_obj(HostScene &s) {
+    const uint32_t nv = static_cast<uint32_t>(s.verts.size() / 3);
+    size_t k = 0;
+    for (size_t i = 0; i < s.tri_mat.size(); ++i) {
+        if (s.tris[3 * i] < nv && s.tris[3 * i + 1] < nv && s.tris[3 * i + 2] < nv) {
+            s.tris[3 * k] = s.tris[3 * i]; s.tris[3 * k + 1] = s.tris[3 * i + 1]; s.tris[3 * k + 2] = s.tris[3 * i + 2];
+            s.tri_mat[k] = s.tri_mat[i];
+            ++k;
+        }
+    }
+    s.tris.resize(3 * k);
+    s.tri_mat.resize(k);
+    compute_face_normals(s);
+}
+
+int load_obj(const char *path, HostScene &s, std::string &err) {
+    s = HostScene();
+    FILE *in = std::fopen(path, "r");
+    if (!in) {
+        err = std::string("cannot open OBJ file '") + path + "'";
+        return RT_E_IO;
+    }
+    ObjControlState cs(path, s);
     char line[kLineLen];
-    std::string matname;
     float x = 0, y = 0, z = 0;
     std::vector<int> vh;
     vh.reserve(64);
@@ -163,8 +210,7 @@ int load_obj(const char *path, HostScene &s, std::string &err) {
                 ++component;
                 if (endOfVertex) { component = 0; endOfVertex = false; }
             }
-            int m = matname.empty() ? -1 : index.find(matname);
-            if (m < 0) m = 0;
+            const int m = cs.current_material();
             bool bad = false;
             for (int v : vh) bad |= (v < 0);
             if (!bad) {
@@ -179,42 +225,15 @@ int load_obj(const char *path, HostScene &s, std::string &err) {
                 }
             }
         } else if (std::strncmp(line, "mtllib ", 7) == 0) {
-            char *p0 = line + 6;
-            while (std::isspace(static_cast<unsigned char>(*++p0))) {}
-            size_t i = 0;
-            while (p0[i] && !(static_cast<signed char>(p0[i]) < 32)) ++i;
-            prefix.append(p0, i);      // path_.append(...) mutates the prefix (mesh.cpp:173-175)
-            load_mtl(prefix, s, index);
+            cs.mtllib(line);
         } else if (std::strncmp(line, "usemtl ", 7) == 0) {
-            char *p0 = line + 6;
-            while (std::isspace(static_cast<unsigned char>(*++p0))) {}
-            char *p1 = p0;
-            while (*p1 && !std::isspace(static_cast<unsigned char>(*p1))) ++p1;
-            matname.assign(p0, p1);
-            if (index.find(matname) < 0) {
-                std::fprintf(stderr, "Warning! Material '%s' not defined in material file. Taking default!\n",
-                             matname.c_str());
-                matname.clear();
-            }
+            cs.usemtl(line);
         }
         // `vt`, `vn`, `o`, `g`, `s`: not used by the tracer
         std::memset(line, 0, kLineLen);
     }
     std::fclose(in);
-
-    // drop triangles referencing non-existent vertices (reference: out-of-bounds read)
-    const uint32_t nv = static_cast<uint32_t>(s.verts.size() / 3);
-    size_t k = 0;
-    for (size_t i = 0; i < s.tri_mat.size(); ++i) {
-        if (s.tris[3 * i] < nv && s.tris[3 * i + 1] < nv && s.tris[3 * i + 2] < nv) {
-            s.tris[3 * k] = s.tris[3 * i]; s.tris[3 * k + 1] = s.tris[3 * i + 1]; s.tris[3 * k + 2] = s.tris[3 * i + 2];
-            s.tri_mat[k] = s.tri_mat[i];
-            ++k;
-        }
-    }
-    s.tris.resize(3 * k);
-    s.tri_mat.resize(k);
-    compute_face_normals(s);
+    finish_obj(s);
     return RT_OK;
 }
 
