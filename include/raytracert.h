@@ -161,6 +161,9 @@ int rt_scene_get_accel(const rt_scene *scene, int32_t *mode);
  * four-wide tree the kernels traverse by default, [6] its depth. Builds the BVH on demand. */
 #define RT_BVH_INFO_FIELDS 7
 int rt_scene_bvh_info(rt_scene *scene, int32_t info[RT_BVH_INFO_FIELDS]);
+/* 64-bit FNV-1a digest of the BVH arrays the device receives (both trees, leaf order, always
+ * list): equal digests = identical trees (the parallel and sequential builds are compared so). */
+int rt_scene_bvh_digest(rt_scene *scene, uint64_t *digest);
 /* Host-side structural check of the built BVH (containment, coverage, depth bound). */
 int rt_scene_bvh_validate(rt_scene *scene);
 /* The padded acceptance box of one triangle T = {T0, T1, T2} (9 floats), as the BVH uses it.

@@ -89,6 +89,7 @@ _SIGNATURES = {
     "rt_scene_get_accel": ([_VP, C.POINTER(C.c_int32)], C.c_int),
     "rt_scene_bvh_info": ([_VP, _VP], C.c_int),
     "rt_work_detail": ([_VP, C.c_int32, _VP], C.c_int),
+    "rt_scene_bvh_digest": ([_VP, C.POINTER(C.c_uint64)], C.c_int),
     "rt_scene_bvh_validate": ([_VP], C.c_int),
     "rt_bvh_acceptance_box": ([_VP, _VP, _VP], C.c_int),
     "rt_scene_tune": ([_VP, C.c_int32, C.c_int32], C.c_int),

@@ -222,6 +222,12 @@ class Scene:
              "pipes": _capi.TUNE_PIPES}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
 
+    def bvh_digest(self) -> int:
+        """FNV-1a digest of the device BVH arrays (identical trees <=> equal digests)."""
+        d = C.c_uint64()
+        check(lib().rt_scene_bvh_digest(self._h, C.byref(d)))
+        return d.value
+
     def bvh_validate(self) -> None:
         check(lib().rt_scene_bvh_validate(self._h))
 

@@ -30,8 +30,12 @@
 // tests/test_bvh.py checks the acceptance claim directly against the oracle's arithmetic, and
 // tests/test_gpu_parity.py checks BVH results against brute force bit for bit.
 #include <algorithm>
+#include <array>
+#include <atomic>
+#include <thread>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -81,23 +85,47 @@ inline float down(double v) { float f = static_cast<float>(v); return (static_ca
 inline float up(double v) { float f = static_cast<float>(v); return (static_cast<double>(f) < v) ? std::nextafter(f, FLT_MAX) : f; }
 
 struct Builder {
-    std::vector<BuildPrim> prims;
+    std::vector<BuildPrim> &prims;
     std::vector<BuildNode> nodes;
     int max_depth = 0;
 
-    int build(int first, int count, int depth) {
+    explicit Builder(std::vector<BuildPrim> &p) : prims(p) {}
+
+    // One node over prims[first, first + count): its box, and either a leaf (returns -1) or the
+    // binned-SAH split position with the range partitioned around it (returns mid).
+    int threads = 1;   // > 1: the scans over one node's prims are split (top of the tree only)
+
+    // Apply fn(begin, end, part) over [first, first + count) in `parts` contiguous parts.
+    template <typename F>
+    void split_scan(int first, int count, int parts, F &&fn) {
+        if (parts <= 1) { fn(first, first + count, 0); return; }
+        std::vector<std::thread> pool;
+        for (int t = 1; t < parts; ++t)
+            pool.emplace_back([&, t]() { fn(first + int(int64_t(count) * t / parts), first + int(int64_t(count) * (t + 1) / parts), t); });
+        fn(first, first + int(int64_t(count) / parts), 0);
+        for (auto &th : pool) th.join();
+    }
+
+    int make_node(int first, int count, int depth, int &id) {
+        // min/max boxes and bin counts are order-independent, so splitting the scans changes nothing
+        const int parts = (threads > 1 && count >= (1 << 17)) ? threads : 1;
         BuildNode n;
-        for (int i = 0; i < count; ++i) n.box.grow(prims[first + i].box);
-        const int id = static_cast<int>(nodes.size());
+        Box cb;
+        {
+            std::vector<Box> pb(parts), pc(parts);
+            split_scan(first, count, parts, [&](int a, int e, int t) {
+                for (int i = a; i < e; ++i) { pb[t].grow(prims[i].box); pc[t].grow(prims[i].centroid); }
+            });
+            for (int t = 0; t < parts; ++t) { n.box.grow(pb[t]); cb.grow(pc[t]); }
+        }
+        id = static_cast<int>(nodes.size());
         nodes.push_back(n);
         max_depth = std::max(max_depth, depth);
         if (count <= kMaxLeaf || depth >= kMaxBvhDepth - 1) {
             nodes[id].first = first;
             nodes[id].count = count;
-            return id;
+            return -1;
         }
-        Box cb;
-        for (int i = 0; i < count; ++i) cb.grow(prims[first + i].centroid);
         int best_axis = -1, best_split = -1;
         double best_cost = static_cast<double>(count) * n.box.area();   // cost of a leaf (intersection-only SAH)
         for (int axis = 0; axis < 3; ++axis) {
@@ -105,11 +133,20 @@ struct Builder {
             if (!(ext > 0)) continue;
             Box bb[kBins];
             int bc[kBins] = {0};
-            for (int i = 0; i < count; ++i) {
-                int b = static_cast<int>((prims[first + i].centroid[axis] - lo) / ext * kBins);
-                b = std::min(std::max(b, 0), kBins - 1);
-                bb[b].grow(prims[first + i].box);
-                bc[b]++;
+            {
+                std::vector<std::array<Box, kBins>> pbb(parts);
+                std::vector<std::array<int, kBins>> pbc(parts);
+                split_scan(first, count, parts, [&](int a, int e, int t) {
+                    pbc[t].fill(0);
+                    for (int i = a; i < e; ++i) {
+                        int b = static_cast<int>((prims[i].centroid[axis] - lo) / ext * kBins);
+                        b = std::min(std::max(b, 0), kBins - 1);
+                        pbb[t][b].grow(prims[i].box);
+                        pbc[t][b]++;
+                    }
+                });
+                for (int t = 0; t < parts; ++t)
+                    for (int b = 0; b < kBins; ++b) { bb[b].grow(pbb[t][b]); bc[b] += pbc[t][b]; }
             }
             Box left[kBins];
             int lc[kBins];
@@ -131,7 +168,7 @@ struct Builder {
             if (count <= 2 * kMaxLeaf) {   // no useful split: small leaf
                 nodes[id].first = first;
                 nodes[id].count = count;
-                return id;
+                return -1;
             }
             // degenerate centroids: median split on the widest box axis
             int axis = 0;
@@ -150,11 +187,62 @@ struct Builder {
             mid = static_cast<int>(it - prims.begin());
             if (mid == first || mid == first + count) mid = first + count / 2;
         }
+        return mid;
+    }
+
+    int build(int first, int count, int depth) {
+        int id;
+        const int mid = make_node(first, count, depth, id);
+        if (mid < 0) return id;
         const int l = build(first, mid - first, depth + 1);
         const int r = build(mid, first + count - mid, depth + 1);
         nodes[id].left = l;
         nodes[id].right = r;
         return id;
+    }
+
+    // The same tree, built by `threads` threads: the top levels are split here until there are
+    // about four subtrees per thread, then each subtree is built by its own Builder over its
+    // disjoint prim range and spliced in. Every node makes the decision the sequential build
+    // makes on the same range, so the flattened tree is identical.
+    void build_parallel(int count, int threads) {
+        struct Task { int first, count, depth, parent; bool right; };
+        std::vector<Task> todo, frontier{Task{0, count, 0, -1, false}};
+        this->threads = threads;
+        const int grain = std::max(4096, count / (4 * std::max(threads, 1)));
+        while (!frontier.empty()) {
+            const Task t = frontier.back();
+            frontier.pop_back();
+            if (t.count <= grain) { todo.push_back(t); continue; }
+            int id;
+            const int mid = make_node(t.first, t.count, t.depth, id);
+            if (t.parent >= 0) (t.right ? nodes[t.parent].right : nodes[t.parent].left) = id;
+            if (mid < 0) continue;
+            frontier.push_back(Task{mid, t.first + t.count - mid, t.depth + 1, id, true});
+            frontier.push_back(Task{t.first, mid - t.first, t.depth + 1, id, false});
+        }
+        std::vector<Builder> sub;
+        sub.reserve(todo.size());
+        for (size_t i = 0; i < todo.size(); ++i) sub.emplace_back(prims);
+        std::vector<int> root(todo.size(), -1);
+        std::atomic<size_t> next{0};
+        auto worker = [&]() {
+            for (size_t i; (i = next.fetch_add(1)) < todo.size();) root[i] = sub[i].build(todo[i].first, todo[i].count, todo[i].depth);
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < threads; ++t) pool.emplace_back(worker);
+        worker();
+        for (auto &th : pool) th.join();
+        for (size_t i = 0; i < todo.size(); ++i) {
+            const int off = static_cast<int>(nodes.size());
+            for (BuildNode n : sub[i].nodes) {
+                if (n.left >= 0) { n.left += off; n.right += off; }
+                nodes.push_back(n);
+            }
+            const int r = root[i] + off;
+            if (todo[i].parent >= 0) (todo[i].right ? nodes[todo[i].parent].right : nodes[todo[i].parent].left) = r;
+            max_depth = std::max(max_depth, sub[i].max_depth);
+        }
     }
 };
 
@@ -279,27 +367,38 @@ bool acceptance_box(const TriRec &T, const float *v0, const float *v1, const flo
 int build_bvh(const HostScene &s, const std::vector<TriRec> &recs, HostBvh &out) {
     out = HostBvh();
     const size_t nt = recs.size();
-    Builder b;
-    b.prims.reserve(nt);
+    std::vector<BuildPrim> prims;
+    Builder b(prims);
+    int threads = static_cast<int>(std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+    if (const char *e = std::getenv("RTAMD_BVH_THREADS")) threads = std::max(1, std::atoi(e));   // diagnostics / tests
     double m1 = 0;
     for (size_t i = 0; i < s.verts.size() / 3; ++i)
         m1 = std::max(m1, std::fabs(double(s.verts[3 * i])) + std::fabs(double(s.verts[3 * i + 1])) + std::fabs(double(s.verts[3 * i + 2])));
     out.scene_m1 = static_cast<float>(m1 * (1 + 1e-6));
-    for (size_t i = 0; i < nt; ++i) {
-        const float *v0 = &s.verts[3 * s.tris[3 * i]];
-        const float *v1 = &s.verts[3 * s.tris[3 * i + 1]];
-        const float *v2 = &s.verts[3 * s.tris[3 * i + 2]];
-        BuildPrim p;
-        bool never = false;
-        if (!acceptance_box(recs[i], v0, v1, v2, p.box.lo, p.box.hi, &never)) {
-            out.always.push_back(static_cast<uint32_t>(i));
-            continue;
+    // acceptance boxes in parallel, then the lists in triangle order
+    std::vector<BuildPrim> all(nt);
+    std::vector<uint8_t> kind(nt);   // 0 tree, 1 always list, 2 never accepted
+    b.split_scan(0, static_cast<int>(nt), nt >= 65536 ? threads : 1, [&](int a, int e, int) {
+        for (int i = a; i < e; ++i) {
+            const float *v0 = &s.verts[3 * s.tris[3 * i]];
+            const float *v1 = &s.verts[3 * s.tris[3 * i + 1]];
+            const float *v2 = &s.verts[3 * s.tris[3 * i + 2]];
+            BuildPrim &p = all[i];
+            bool never = false;
+            if (!acceptance_box(recs[i], v0, v1, v2, p.box.lo, p.box.hi, &never)) { kind[i] = 1; continue; }
+            if (never) { kind[i] = 2; continue; }
+            kind[i] = 0;
+            for (int k = 0; k < 3; ++k) p.centroid[k] = 0.5f * (p.box.lo[k] + p.box.hi[k]);
+            p.tri = static_cast<uint32_t>(i);
         }
-        if (never) { out.n_never++; continue; }
-        for (int k = 0; k < 3; ++k) p.centroid[k] = 0.5f * (p.box.lo[k] + p.box.hi[k]);
-        p.tri = static_cast<uint32_t>(i);
-        b.prims.push_back(p);
+    });
+    prims.reserve(nt);
+    for (size_t i = 0; i < nt; ++i) {
+        if (kind[i] == 0) prims.push_back(all[i]);
+        else if (kind[i] == 1) out.always.push_back(static_cast<uint32_t>(i));
+        else out.n_never++;
     }
+    std::vector<BuildPrim>().swap(all);
     const int np = static_cast<int>(b.prims.size());
     if (np == 0) {
         BvhNode root{};
@@ -312,7 +411,8 @@ int build_bvh(const HostScene &s, const std::vector<TriRec> &recs, HostBvh &out)
         out.depth4 = 1;
         return RT_OK;
     }
-    b.build(0, np, 0);
+    if (np > 65536 && threads > 1) b.build_parallel(np, threads);
+    else b.build(0, np, 0);
     out.depth = b.max_depth + 1;
     // leaf order
     out.leaf_tris.resize(np);
@@ -493,6 +593,19 @@ int validate_bvh(const HostScene &s, const std::vector<TriRec> &recs, const Host
     if (inner_seen != h.nodes.size()) { err = "unreachable nodes"; return RT_E_PARSE; }
     if (never != h.n_never) { err = "degenerate count mismatch"; return RT_E_PARSE; }
     return validate_bvh4(s, recs, h, err);
+}
+
+uint64_t bvh_digest(const HostBvh &h) {
+    uint64_t x = 1469598103934665603ull;   // FNV-1a over the arrays the device receives
+    auto mix = [&](const void *p, size_t n) {
+        const unsigned char *c = static_cast<const unsigned char *>(p);
+        for (size_t i = 0; i < n; ++i) { x ^= c[i]; x *= 1099511628211ull; }
+    };
+    mix(h.nodes.data(), h.nodes.size() * sizeof(BvhNode));
+    mix(h.nodes4.data(), h.nodes4.size() * sizeof(Bvh4Node));
+    mix(h.leaf_tris.data(), h.leaf_tris.size() * sizeof(uint32_t));
+    mix(h.always.data(), h.always.size() * sizeof(uint32_t));
+    return x;
 }
 
 }  // namespace rt

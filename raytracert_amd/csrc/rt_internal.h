@@ -103,6 +103,7 @@ bool acceptance_box(const TriRec &T, const float *v0, const float *v1, const flo
                     bool *never);
 int build_bvh(const HostScene &s, const std::vector<TriRec> &recs, HostBvh &out);
 float bvh4_decode(float origin, int ex, uint32_t q);
+uint64_t bvh_digest(const HostBvh &h);
 int validate_bvh(const HostScene &s, const std::vector<TriRec> &recs, const HostBvh &h, std::string &err);
 
 // OBJ reader material state shared by the sequential and the parallel parser (scene_loader.cpp).

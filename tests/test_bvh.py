@@ -155,3 +155,17 @@ def test_quantised_boxes_on_far_flat_and_tiny_geometry(tmp_path):
     s.bvh_validate()
     info = s.bvh_info()
     assert info["nodes4"] >= 1 and info["leaf_triangles"] + info["always"] + info["never"] == 720
+
+
+def test_parallel_build_is_the_sequential_tree(workdir, monkeypatch):
+    """The threaded build (top levels split with parallel scans, subtrees on worker threads) makes
+    every node decision the sequential build makes on the same prim range: identical device arrays
+    (digest over both trees, the leaf order and the always list)."""
+    path = scene_path("syn:C4", workdir)
+    digests = {}
+    for t in ("1", "3", "8"):
+        monkeypatch.setenv("RTAMD_BVH_THREADS", t)
+        s = R.Scene.load(path, device=R.RT_HOST_ONLY)
+        digests[t] = s.bvh_digest()
+        s.bvh_validate()
+    assert len(set(digests.values())) == 1, digests
