@@ -12,6 +12,7 @@
  *   rt_get_material       Material getMaterial(int)         raytracing.h:27, raytracing.cpp:373-376
  *   rt_intersect_mesh     intersectMesh (batched)           raytracing.cpp:161-192
  *   rt_trace_rays         Vec3Df performRayTracing(o, d)    raytracing.h:33, raytracing.cpp:410-416
+ *   rt_debug_trace        debug key 'd' (shoot + trace)     raytracing.cpp:493-510
  *                         (batched; also trace(o,d,lvl) at lvl 0, raytracing.h:30)
  *   rt_render_tile        the 'r'-key frame loop            main.cpp:340-411 (loop :355-395,
  *                         + RGBValue clamp :24-42 + Image::writeImage quantisation :102-128)
@@ -51,6 +52,15 @@ extern "C" {
 #define RT_SHADOWS    (1u << 4)
 #define RT_REFRACTION (1u << 5)
 #define RT_ALL_FEATURES 0x3Fu
+/* Extension (the reference has only the regular pf x pf grid): each sub-sample
+ * is jittered inside its grid cell by a counter-based hash of (pixel, sub-sample, seed), so a
+ * stochastic frame is still a pure function of its parameters and the CPU restatement checks it
+ * bit for bit. Sub-sample (subx, suby) of pixel (x, y): key = (y*width + x)*pfx*pfy + subx*pfy +
+ * suby; h1 = fmix32(key ^ fmix32(seed)), h2 = fmix32(h1 + 0x9E3779B9) (MurmurHash3 finaliser);
+ * jx = (h1 >> 8) * 2^-24, jy = (h2 >> 8) * 2^-24; xscale = 1 - (x*pfx + (subx + jx)) / divX and
+ * likewise y, every operation in binary32. */
+#define RT_STOCHASTIC (1u << 8)
+#define RT_DEFAULT_SEED 0x5EED
 
 /* Material "is set" flags (mesh.h:116-122). */
 #define RT_HAS_KD    (1u << 0)
@@ -79,7 +89,7 @@ typedef struct {
     int32_t max_lvl;              /* max recursion level (raytracing.cpp:29), >= 0 */
     uint32_t flags;               /* RT_AMBIENT ... RT_REFRACTION */
     int32_t n_lights;             /* MyLightPositions.size(), 0..RT_MAX_LIGHTS */
-    int32_t reserved;             /* must be 0 */
+    int32_t seed;                 /* RT_STOCHASTIC only (else ignored): jitter hash seed */
     float lights[RT_MAX_LIGHTS][3];
     float camera_pos[3];          /* MyCameraPosition (raytracing.h:10) */
     float corners[8][3];          /* origin00,dest00, origin01,dest01, origin10,dest10, origin11,dest11 */
@@ -123,6 +133,22 @@ int rt_intersect_mesh(rt_scene *scene, const float *origins, const float *dests,
  * counts (may be NULL) receives {primary, secondary, shadow} intersectMesh-equivalent queries. */
 int rt_trace_rays(rt_scene *scene, const rt_params *params, const float *origins, const float *dests,
                   int32_t n, float *rgb_out, uint64_t counts[3]);
+
+/* Single-ray debug trace (the reference's key 'd', raytracing.cpp:493-510, which shoots one ray,
+ * keeps (origin, intersection) for drawing and prints the traced colour): one record per trace()
+ * call of the ray's chain, in order, with the outcome of each shadow ray its shade() cast. For
+ * parity triage: compare against the oracle's ora_debug_trace to find the first bounce that
+ * differs. Writes min(n, max_bounces) records; *n_bounces = n; rgb = performRayTracing(o, d). */
+typedef struct {
+    float origin[3], dest[3];     /* the ray trace() was called with */
+    float hit[3];                 /* intersectMesh's point, (0,0,0) on a miss */
+    int32_t triangle;             /* intersectMesh's index, -1 on a miss */
+    int32_t level;                /* trace()'s lvl argument */
+    uint32_t shadowed;            /* bit l: light l's shadow ray was blocked (isShadow true) */
+    uint32_t lit;                 /* bit l: light l's shadow ray was traced and not blocked */
+} rt_debug_bounce;
+int rt_debug_trace(rt_scene *scene, const rt_params *params, const float origin[3], const float dest[3],
+                   rt_debug_bounce *bounces, int32_t max_bounces, int32_t *n_bounces, float rgb[3]);
 /* The frame loop for pixels [x0,x0+w) x [y0,y0+h) of the params->width x params->height frame.
  * rgb_u8 (w*h*3 bytes, row-major, top row first, as written to result.ppm) and rgb_f32
  * (w*h*3 clamped floats) are host buffers; either may be NULL. */

@@ -22,7 +22,7 @@ class OraParams(C.Structure):
         ("width", C.c_int32), ("height", C.c_int32),
         ("pfx", C.c_int32), ("pfy", C.c_int32),
         ("max_lvl", C.c_int32), ("flags", C.c_uint32),
-        ("n_lights", C.c_int32), ("reserved", C.c_int32),
+        ("n_lights", C.c_int32), ("seed", C.c_int32),
         ("lights", (C.c_float * 3) * MAX_LIGHTS),
         ("camera_pos", C.c_float * 3),
         ("corners", (C.c_float * 3) * 8),
@@ -60,6 +60,8 @@ def lib():
         L.ora_render.argtypes = [C.c_void_p, C.POINTER(OraParams), C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                  C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
         L.ora_default_corners.argtypes = [C.c_int32, C.c_int32, C.c_void_p]
+        L.ora_debug_trace.argtypes = [C.c_void_p, C.POINTER(OraParams), C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+        L.ora_debug_trace.restype = C.c_int32
         _lib = L
     return _lib
 
@@ -74,11 +76,23 @@ def default_corners(width: int, height: int) -> np.ndarray:
     return out
 
 
+STOCHASTIC = 1 << 8      # RT_STOCHASTIC: jittered sub-samples (include/raytracert.h)
+DEFAULT_SEED = 0x5EED
+
+
+class OraDebugBounce(C.Structure):
+    _fields_ = [
+        ("origin", C.c_float * 3), ("dest", C.c_float * 3), ("hit", C.c_float * 3),
+        ("triangle", C.c_int32), ("level", C.c_int32), ("shadowed", C.c_uint32), ("lit", C.c_uint32),
+    ]
+
+
 def make_params(width, height, pf=1, max_lvl=0, lights=((0.0, 0.0, 4.0),), flags=ALL_FEATURES,
-                camera_pos=(0.0, 0.0, 4.0), corners=None) -> OraParams:
+                camera_pos=(0.0, 0.0, 4.0), corners=None, seed=DEFAULT_SEED) -> OraParams:
     p = OraParams()
     p.width, p.height, p.pfx, p.pfy = width, height, pf, pf
     p.max_lvl, p.flags, p.n_lights = max_lvl, flags, len(lights)
+    p.seed = seed
     for i, l in enumerate(lights):
         for k in range(3):
             p.lights[i][k] = l[k]
@@ -138,6 +152,21 @@ class OracleScene:
         counts = np.zeros(3, np.uint64)
         lib().ora_perform_ray_tracing(self.h, C.byref(params), _ptr(o), _ptr(d), _ptr(rgb), _ptr(counts))
         return rgb, counts
+
+    def debug_trace(self, params: OraParams, origin, dest, max_bounces=256):
+        """Every trace() call of one ray's chain (ora_debug_trace): (bounces, rgb), bounces as
+        dicts with the fields of rt_debug_bounce."""
+        buf = (OraDebugBounce * max_bounces)()
+        rgb = np.zeros(3, np.float32)
+        o = np.ascontiguousarray(origin, np.float32).reshape(3)
+        d = np.ascontiguousarray(dest, np.float32).reshape(3)
+        n = lib().ora_debug_trace(self.h, C.byref(params), _ptr(o), _ptr(d), buf, max_bounces, _ptr(rgb))
+        out = []
+        for b in buf[: min(n, max_bounces)]:
+            out.append(dict(origin=np.array(b.origin[:], np.float32), dest=np.array(b.dest[:], np.float32),
+                            hit=np.array(b.hit[:], np.float32), triangle=b.triangle, level=b.level,
+                            shadowed=b.shadowed, lit=b.lit))
+        return out, rgb
 
     def render(self, params: OraParams, x0=0, y0=0, w=None, h=None, nthreads=None):
         w = params.width if w is None else w

@@ -387,6 +387,8 @@ typedef struct {
     const ora_scene *sc;
     const ora_params *pr;
     uint64_t n_primary, n_secondary, n_shadow;
+    ora_debug_bounce *dbg;   /* ora_debug_trace: one record per trace() call, in call order */
+    int dbg_max, dbg_n, cur_light;
 } ctx;
 
 static vec3 trace(ctx *c, vec3 origin, vec3 dest, int lvl);
@@ -426,10 +428,17 @@ static int is_shadow(ctx *c, vec3 intersection, vec3 light_pos) {
         intersection = vadd(intersection, V(0.1f, 0.1f, 0.1f));
         c->n_shadow++;
         int index = intersect_mesh(c->sc, intersection, light_pos, &out2);
-        if (index == -1) return 0;
-        const material *m = &c->sc->mats[c->sc->tmat[index]];   /* getMaterial, :373-376 */
-        if ((m->flags & ORA_HAS_TR) && m->Tr < 1.0f) return 0;
-        return 1;
+        int blocked = 1;
+        if (index == -1) blocked = 0;
+        else {
+            const material *m = &c->sc->mats[c->sc->tmat[index]];   /* getMaterial, :373-376 */
+            if ((m->flags & ORA_HAS_TR) && m->Tr < 1.0f) blocked = 0;
+        }
+        if (c->dbg && c->dbg_n >= 1 && c->dbg_n <= c->dbg_max) {
+            ora_debug_bounce *b = &c->dbg[c->dbg_n - 1];   /* the trace whose shade() asks */
+            if (blocked) b->shadowed |= 1u << c->cur_light; else b->lit |= 1u << c->cur_light;
+        }
+        return blocked;
     }
     return 0;
 }
@@ -493,6 +502,7 @@ static vec3 shade(ctx *c, vec3 ray, vec3 vertexPos, vec3 *normal, const material
     if (feat(c, ORA_AMBIENT) && (m->flags & ORA_HAS_KA)) pixelcolor = vadd(pixelcolor, m->Ka);
     for (int i = 0; i < c->pr->n_lights; i++) {
         vec3 L = V(c->pr->lights[i][0], c->pr->lights[i][1], c->pr->lights[i][2]);
+        c->cur_light = i;
         if (!is_shadow(c, vertexPos, L)) {
             if (feat(c, ORA_DIFFUSE) && (m->flags & ORA_HAS_KD))
                 pixelcolor = vadd(pixelcolor, vscale(diffuse_only(m, normal, L), m->Tr));
@@ -513,6 +523,17 @@ static vec3 trace(ctx *c, vec3 origin, vec3 dest, int lvl) {
     vec3 intersectOut;
     if (lvl == 0) c->n_primary++; else c->n_secondary++;
     int index = intersect_mesh(c->sc, origin, dest, &intersectOut);
+    if (c->dbg) {
+        if (c->dbg_n < c->dbg_max) {
+            ora_debug_bounce *b = &c->dbg[c->dbg_n];
+            memset(b, 0, sizeof *b);
+            memcpy(b->origin, origin.p, 12); memcpy(b->dest, dest.p, 12);
+            if (index != -1) memcpy(b->hit, intersectOut.p, 12);
+            b->triangle = index;
+            b->level = lvl;
+        }
+        c->dbg_n++;
+    }
     if (index == -1) return pixelcolor;
     vec3 ray = vsub(dest, origin);
     vec3 normal = c->sc->normals[index];
@@ -543,9 +564,19 @@ int ora_intersect_mesh(const ora_scene *s, const float origin[3], const float de
     return idx;
 }
 
+/* Single-ray debug trace (reference key 'd', raytracing.cpp:493-510): every trace() call of the
+ * chain in order, with its shadow-ray outcomes. Returns the number of trace() calls. */
+int ora_debug_trace(const ora_scene *s, const ora_params *p, const float o[3], const float d[3],
+                    ora_debug_bounce *out, int32_t max_bounces, float rgb[3]) {
+    ctx c = {s, p, 0, 0, 0, out, max_bounces, 0, 0};
+    vec3 col = trace(&c, V(o[0], o[1], o[2]), V(d[0], d[1], d[2]), 0);
+    memcpy(rgb, col.p, 12);
+    return c.dbg_n;
+}
+
 void ora_perform_ray_tracing(const ora_scene *s, const ora_params *p, const float o[3], const float d[3],
                              float rgb[3], uint64_t counts[3]) {
-    ctx c = {s, p, 0, 0, 0};
+    ctx c = {s, p, 0, 0, 0, NULL, 0, 0, 0};
     vec3 col = trace(&c, V(o[0], o[1], o[2]), V(d[0], d[1], d[2]), 0);   /* performRayTracing :410-416 */
     memcpy(rgb, col.p, 12);
     if (counts) { counts[0] += c.n_primary; counts[1] += c.n_secondary; counts[2] += c.n_shadow; }
@@ -558,11 +589,17 @@ typedef struct {
     uint64_t counts[3];
 } render_job;
 
+/* MurmurHash3 32-bit finaliser (public domain algorithm), the jitter hash of RT_STOCHASTIC */
+static uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+    return h;
+}
+
 /* Frame loop of main.cpp:355-395, RGBValue clamp main.cpp:24-42, quantisation main.cpp:116-117 */
 static void *render_rows(void *arg) {
     render_job *j = arg;
     const ora_params *p = j->p;
-    ctx c = {j->s, p, 0, 0, 0};
+    ctx c = {j->s, p, 0, 0, 0, NULL, 0, 0, 0};
     vec3 o00 = V(p->corners[0][0], p->corners[0][1], p->corners[0][2]);
     vec3 d00 = V(p->corners[1][0], p->corners[1][1], p->corners[1][2]);
     vec3 o01 = V(p->corners[2][0], p->corners[2][1], p->corners[2][2]);
@@ -582,8 +619,19 @@ static void *render_rows(void *arg) {
             vec3 rgb = V(0, 0, 0);
             for (int subx = 0; subx < (int)pfx; subx++) {
                 for (int suby = 0; suby < (int)pfy; suby++) {
-                    float xscale = 1.0f - ((float)x * (float)pfx + (float)subx) / divX;
-                    float yscale = 1.0f - ((float)y * (float)pfy + (float)suby) / divY;
+                    float xscale, yscale;
+                    if (p->flags & ORA_STOCHASTIC) {
+                        /* RT_STOCHASTIC (include/raytracert.h): jitter inside the grid cell */
+                        uint32_t key = ((uint32_t)y * (uint32_t)p->width + x) * (pfx * pfy) + (uint32_t)subx * pfy + (uint32_t)suby;
+                        uint32_t h1 = fmix32(key ^ fmix32((uint32_t)p->seed));
+                        uint32_t h2 = fmix32(h1 + 0x9E3779B9u);
+                        float jx = (float)(h1 >> 8) * 0x1p-24f, jy = (float)(h2 >> 8) * 0x1p-24f;
+                        xscale = 1.0f - ((float)x * (float)pfx + ((float)subx + jx)) / divX;
+                        yscale = 1.0f - ((float)y * (float)pfy + ((float)suby + jy)) / divY;
+                    } else {
+                        xscale = 1.0f - ((float)x * (float)pfx + (float)subx) / divX;
+                        yscale = 1.0f - ((float)y * (float)pfy + (float)suby) / divY;
+                    }
                     vec3 origin = vadd(vscale(vadd(vscale(o00, xscale), vscale(o10, 1 - xscale)), yscale),
                                        vscale(vadd(vscale(o01, xscale), vscale(o11, 1 - xscale)), 1 - yscale));
                     vec3 dest = vadd(vscale(vadd(vscale(d00, xscale), vscale(d10, 1 - xscale)), yscale),

@@ -27,6 +27,7 @@ extern "C" {
 #define ORA_SHADOWS    (1u << 4)
 #define ORA_REFRACTION (1u << 5)
 #define ORA_ALL_FEATURES 0x3Fu
+#define ORA_STOCHASTIC (1u << 8)   /* = RT_STOCHASTIC: jittered sub-samples (extension) */
 
 /* Material "is set" bits, mesh.h:116-122. */
 #define ORA_HAS_KD (1u << 0)
@@ -44,7 +45,7 @@ typedef struct {
     int32_t max_lvl;              /* raytracing.cpp:29 */
     uint32_t flags;               /* ORA_AMBIENT ... ORA_REFRACTION */
     int32_t n_lights;             /* MyLightPositions.size() */
-    int32_t reserved;
+    int32_t seed;                 /* with flag bit 8 (RT_STOCHASTIC): jitter seed */
     float lights[ORA_MAX_LIGHTS][3];
     float camera_pos[3];          /* MyCameraPosition */
     float corners[8][3];          /* origin00,dest00, origin01,dest01, origin10,dest10, origin11,dest11 (main.cpp:348-358) */
@@ -76,6 +77,14 @@ void ora_ray_intersect_triangle_batch(const float *R, int32_t n, const float T[9
 /* intersectMesh (raytracing.cpp:161-192). Returns triangle index or -1. */
 int ora_intersect_mesh(const ora_scene *s, const float origin[3], const float dest[3], float I[3]);
 /* performRayTracing (raytracing.cpp:410-416). counts (may be NULL): primary, secondary, shadow queries. */
+/* = rt_debug_bounce (include/raytracert.h) */
+typedef struct {
+    float origin[3], dest[3], hit[3];
+    int32_t triangle, level;
+    uint32_t shadowed, lit;
+} ora_debug_bounce;
+int ora_debug_trace(const ora_scene *s, const ora_params *p, const float o[3], const float d[3],
+                    ora_debug_bounce *out, int32_t max_bounces, float rgb[3]);
 void ora_perform_ray_tracing(const ora_scene *s, const ora_params *p, const float origin[3],
                              const float dest[3], float rgb[3], uint64_t counts[3]);
 /* The 'r' key render loop (main.cpp:355-395) + RGBValue clamp (main.cpp:24-42) + writeImage

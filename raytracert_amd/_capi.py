@@ -33,6 +33,8 @@ KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME = range(4)
 ACCEL_BRUTE_FORCE, ACCEL_BVH = 0, 1
 TUNE_XCD_SPLIT, TUNE_BVH_GRID, TUNE_BVH_WIDTH, TUNE_LDS_STACK, TUNE_PIPES = 0, 1, 2, 3, 4
 BVH_INFO_FIELDS = 7
+STOCHASTIC = 1 << 8
+DEFAULT_SEED = 0x5EED
 LOAD_PARALLEL, LOAD_SEQUENTIAL = 0, 1
 WORK_FIELDS = 6
 
@@ -42,10 +44,17 @@ class RtParams(C.Structure):
         ("width", C.c_int32), ("height", C.c_int32),
         ("pfx", C.c_int32), ("pfy", C.c_int32),
         ("max_lvl", C.c_int32), ("flags", C.c_uint32),
-        ("n_lights", C.c_int32), ("reserved", C.c_int32),
+        ("n_lights", C.c_int32), ("seed", C.c_int32),
         ("lights", (C.c_float * 3) * RT_MAX_LIGHTS),
         ("camera_pos", C.c_float * 3),
         ("corners", (C.c_float * 3) * 8),
+    ]
+
+
+class RtDebugBounce(C.Structure):
+    _fields_ = [
+        ("origin", C.c_float * 3), ("dest", C.c_float * 3), ("hit", C.c_float * 3),
+        ("triangle", C.c_int32), ("level", C.c_int32), ("shadowed", C.c_uint32), ("lit", C.c_uint32),
     ]
 
 
@@ -76,6 +85,7 @@ _SIGNATURES = {
     "rt_get_material": ([_VP, C.c_int32, C.POINTER(RtMaterial)], C.c_int),
     "rt_intersect_mesh": ([_VP, _VP, _VP, C.c_int32, _VP, _VP], C.c_int),
     "rt_trace_rays": ([_VP, C.POINTER(RtParams), _VP, _VP, C.c_int32, _VP, _VP], C.c_int),
+    "rt_debug_trace": ([_VP, C.POINTER(RtParams), _VP, _VP, _VP, C.c_int32, C.POINTER(C.c_int32), _VP], C.c_int),
     "rt_render_tile": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP, _VP, _VP], C.c_int),
     "rt_render_tiles_device": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP,
                                 C.c_size_t, _VP, C.POINTER(C.c_int32), _VP], C.c_int),

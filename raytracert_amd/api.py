@@ -50,6 +50,7 @@ class RenderParams:
     flags: int = ALL_FEATURES
     camera_pos: Sequence[float] = (0.0, 0.0, 4.0)
     corners: np.ndarray | None = field(default=None, repr=False)
+    seed: int = _capi.DEFAULT_SEED   # RT_STOCHASTIC jitter seed (flags | STOCHASTIC)
 
     def to_c(self) -> RtParams:
         if len(self.lights) > _capi.RT_MAX_LIGHTS:
@@ -57,6 +58,7 @@ class RenderParams:
         p = RtParams()
         p.width, p.height, p.pfx, p.pfy = self.width, self.height, self.pf, self.pf
         p.max_lvl, p.flags, p.n_lights = self.max_lvl, self.flags, len(self.lights)
+        p.seed = int(self.seed)
         for i, l in enumerate(self.lights):
             for k in range(3):
                 p.lights[i][k] = float(l[k])
@@ -171,6 +173,25 @@ class Scene:
         p = params.to_c()
         check(lib().rt_trace_rays(self._h, C.byref(p), _ptr(o), _ptr(d), n, _ptr(rgb), _ptr(counts)))
         return rgb, counts
+
+    def debug_trace(self, params: RenderParams, origin, dest, max_bounces: int = 256):
+        """The debug key 'd' (raytracing.cpp:493-510) for one ray: (bounces, rgb). Each bounce is
+        a dict (origin, dest, hit, triangle, level, shadowed, lit) for one trace() call, in
+        order; rgb = performRayTracing(origin, dest)."""
+        from ._capi import RtDebugBounce
+        buf = (RtDebugBounce * max_bounces)()
+        n = C.c_int32()
+        rgb = np.zeros(3, np.float32)
+        o = np.ascontiguousarray(origin, np.float32).reshape(3)
+        d = np.ascontiguousarray(dest, np.float32).reshape(3)
+        p = params.to_c()
+        check(lib().rt_debug_trace(self._h, C.byref(p), _ptr(o), _ptr(d), buf, max_bounces, C.byref(n), _ptr(rgb)))
+        out = []
+        for b in buf[: min(n.value, max_bounces)]:
+            out.append(dict(origin=np.array(b.origin[:], np.float32), dest=np.array(b.dest[:], np.float32),
+                            hit=np.array(b.hit[:], np.float32), triangle=b.triangle, level=b.level,
+                            shadowed=b.shadowed, lit=b.lit))
+        return out, rgb
 
     def render(self, params: RenderParams, x0: int = 0, y0: int = 0, w: int | None = None, h: int | None = None,
                want_f32: bool = False):

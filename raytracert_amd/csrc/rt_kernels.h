@@ -23,6 +23,8 @@ struct FrameGeom {
     int32_t ox, oy, cw, ch;             // tiled region origin / clip size (absolute pixels)
     int32_t out_mode;                   // 0: tile-major shard layout, 1: row-major in the clip rect
     int32_t tiles_total;                // tiles per frame: ids wrap modulo this (multi-frame batches)
+    int32_t stochastic;                 // RT_STOCHASTIC: jittered sub-samples
+    uint32_t seed;                      // its hash seed
     float corners[8][3];                // origin00,dest00,origin01,dest01,origin10,dest10,origin11,dest11
 };
 

@@ -693,6 +693,12 @@ __device__ __forceinline__ bool decode_pixel(const FrameGeom &g, int64_t pix, in
 
 // The primary queue is dense: query s is sample s, so no compaction (and no atomics) at all;
 // samples outside the frame or the clip rectangle are marked inactive with lvl = -1.
+// MurmurHash3 32-bit finaliser (the RT_STOCHASTIC jitter hash; oracle/rt_oracle.c has the same)
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+    return h;
+}
+
 __global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWork w) {
     const int spp = g.pfx * g.pfy;
     const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th * spp;
@@ -706,8 +712,17 @@ __global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWo
     const bool valid = decode_pixel(g, pix, x, y);
     V3 origin = mk(0, 0, 0), dest = mk(0, 0, 0);
     if (valid) {
-        const float xscale = 1.0f - (static_cast<float>(static_cast<unsigned>(x)) * static_cast<float>(static_cast<unsigned>(g.pfx)) + static_cast<float>(subx)) / g.divX;  // :380
-        const float yscale = 1.0f - (static_cast<float>(static_cast<unsigned>(y)) * static_cast<float>(static_cast<unsigned>(g.pfy)) + static_cast<float>(suby)) / g.divY;  // :381
+        float fx = static_cast<float>(subx), fy = static_cast<float>(suby);
+        if (g.stochastic) {   // RT_STOCHASTIC (include/raytracert.h): jitter inside the grid cell
+            const uint32_t key = (static_cast<uint32_t>(y) * static_cast<uint32_t>(g.width) + static_cast<uint32_t>(x)) *
+                                     static_cast<uint32_t>(spp) + static_cast<uint32_t>(sub);
+            const uint32_t h1 = fmix32(key ^ fmix32(g.seed));
+            const uint32_t h2 = fmix32(h1 + 0x9E3779B9u);
+            fx = fx + static_cast<float>(h1 >> 8) * 0x1p-24f;
+            fy = fy + static_cast<float>(h2 >> 8) * 0x1p-24f;
+        }
+        const float xscale = 1.0f - (static_cast<float>(static_cast<unsigned>(x)) * static_cast<float>(static_cast<unsigned>(g.pfx)) + fx) / g.divX;  // :380
+        const float yscale = 1.0f - (static_cast<float>(static_cast<unsigned>(y)) * static_cast<float>(static_cast<unsigned>(g.pfy)) + fy) / g.divY;  // :381
         const V3 o00 = mk(g.corners[0][0], g.corners[0][1], g.corners[0][2]);
         const V3 d00 = mk(g.corners[1][0], g.corners[1][1], g.corners[1][2]);
         const V3 o01 = mk(g.corners[2][0], g.corners[2][1], g.corners[2][2]);

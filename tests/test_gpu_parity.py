@@ -288,3 +288,57 @@ def test_launch_shape_knobs_never_change_results(knobs, workdir, gpu_available):
         u8, f32, c = sc.render(p, want_f32=True)
     assert [int(x) for x in c] == [int(x) for x in refc]
     assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
+
+
+@pytest.mark.parametrize("spec,w,h,pf", [("syn:F3", 128, 72, 2), ("syn:F4", 96, 54, 2), ("ref:dodgeColorTest.obj", 80, 60, 3)])
+def test_stochastic_aa_matches_oracle(spec, w, h, pf, workdir, gpu_available):
+    """RT_STOCHASTIC: jittered sub-samples from the counter-based hash of
+    include/raytracert.h. The GPU frame matches the oracle's at the same seed (same query counts,
+    the golden tests' byte and float bar) and differs from the regular-grid frame."""
+    path = scene_path(spec, workdir)
+    lights = [(0.0, 0.0, 4.0), (1.5, 1.5, 4.0)]
+    p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=3, lights=lights, flags=R.ALL_FEATURES | (1 << 8), seed=0x5EED)
+    with R.Scene.load(path, device=0) as sc:
+        u8, f32, counts = sc.render(p, want_f32=True)
+        g8, _, _ = sc.render(R.RenderParams(width=w, height=h, pf=pf, max_lvl=3, lights=lights), want_f32=False)
+    op = O.make_params(w, h, pf=pf, max_lvl=3, lights=lights, flags=O.ALL_FEATURES | O.STOCHASTIC, seed=0x5EED)
+    of32, ou8, ocounts = O.OracleScene(path).render(op)
+    assert [int(c) for c in counts] == [int(c) for c in ocounts]
+    _assert_image_close(u8, f32, ou8, of32)   # the golden-test bar: specular powf may differ by an ulp
+    assert not np.array_equal(u8, g8)
+
+
+@pytest.mark.parametrize("spec", ["syn:F4", "syn:F3", "ref:dodgeColorTest.obj", "ref:Models/shadow_test.obj"])
+def test_debug_trace_matches_oracle(spec, workdir, gpu_available):
+    """rt_debug_trace (the reference's key 'd', raytracing.cpp:493-510): for
+    rays through pixels all over the frame, every trace() call of the chain (ray, hit point,
+    triangle, level, per-light shadow outcome) equals the oracle's record bit for bit, the colour
+    is within the float tolerance of the oracle's and equals performRayTracing's exactly."""
+    path = scene_path(spec, workdir)
+    W, H = 96, 64
+    lights = [(0.0, 0.0, 4.0), (1.5, 1.5, 4.0)]
+    p = R.RenderParams(width=W, height=H, pf=1, max_lvl=6, lights=lights)
+    op = O.make_params(W, H, pf=1, max_lvl=6, lights=lights)
+    cs = R.default_corners(W, H)
+    orc = O.OracleScene(path)
+    rng = np.random.default_rng(3)
+    chains = 0
+    with R.Scene.load(path, device=0) as sc:
+        for _ in range(40):
+            a, b = rng.random(2).astype(np.float32)
+            o = (cs[0] * a + cs[4] * (1 - a)) * b + (cs[2] * a + cs[6] * (1 - a)) * (1 - b)
+            d = (cs[1] * a + cs[5] * (1 - a)) * b + (cs[3] * a + cs[7] * (1 - a)) * (1 - b)
+            gb, grgb = sc.debug_trace(p, o, d)
+            ob, orgb = orc.debug_trace(op, o, d)
+            assert len(gb) == len(ob)
+            for x, y in zip(gb, ob):
+                for k in ("origin", "dest", "hit"):
+                    assert np.array_equal(x[k].view(np.uint32), y[k].view(np.uint32)), (k, x, y)
+                for k in ("triangle", "level", "shadowed", "lit"):
+                    assert x[k] == y[k], (k, x, y)
+            assert np.abs(grgb - orgb).max() <= F32_TOL   # specular powf: at most an ulp apart
+            prgb, _ = sc.perform_ray_tracing(p, o[None], d[None])
+            assert np.array_equal(prgb[0].view(np.uint32), grgb.view(np.uint32))
+            chains += len(gb) > 1
+    if spec.startswith("syn:"):   # the reference models cover a few percent of the default view
+        assert chains > 5

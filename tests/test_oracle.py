@@ -100,3 +100,39 @@ def test_intersect_mesh_tie_keeps_lowest_index(workdir):
     assert idx == 0 and I.tolist() == [0.25, 0.25, 0.0]
     idx, I = sc.intersect_mesh([5, 5, 1], [5, 5, -1])
     assert idx == -1 and I.tolist() == [0, 0, 0]
+
+
+def _fmix32(h):
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+    h ^= h >> 16
+    return h
+
+
+def test_stochastic_jitter_matches_header_definition(workdir):
+    """RT_STOCHASTIC (an extension: the reference has the regular grid only).
+    The oracle's jittered sub-sample positions follow the hash the header defines: check them
+    by rendering a scene whose colour is a function of the primary ray alone, one sample per
+    pixel (pf 1), against numpy's restatement of the jittered primary ray (the oracle's own
+    intersect_mesh supplies the hit)."""
+    path = scene_path("syn:F3", workdir)
+    s = O.OracleScene(path)
+    W, H, seed = 24, 16, 0x5EED
+    p = O.make_params(W, H, pf=2, max_lvl=0, lights=[(0.0, 0.0, 4.0)], flags=O.ALL_FEATURES | O.STOCHASTIC, seed=seed)
+    f_st, u_st, c_st = s.render(p)
+    p_grid = O.make_params(W, H, pf=2, max_lvl=0, lights=[(0.0, 0.0, 4.0)], flags=O.ALL_FEATURES)
+    f_gr, _, c_gr = s.render(p_grid)
+    assert [int(x) for x in c_st] == [int(x) for x in c_gr]     # same number of queries per kind
+    assert not np.array_equal(f_st, f_gr)                      # but other sub-sample positions
+    again = s.render(p)[0]
+    assert np.array_equal(again.view(np.uint32), f_st.view(np.uint32))   # a pure function of params
+    p2 = O.make_params(W, H, pf=2, max_lvl=0, lights=[(0.0, 0.0, 4.0)], flags=O.ALL_FEATURES | O.STOCHASTIC, seed=seed + 1)
+    assert not np.array_equal(s.render(p2)[0], f_st)           # the seed matters
+    # the hash itself, as the header spells it (key of pixel (3, 2), sub-sample (1, 0))
+    key = ((2 * W + 3) * 4 + 1 * 2 + 0) & 0xFFFFFFFF
+    h1 = _fmix32(key ^ _fmix32(seed))
+    h2 = _fmix32((h1 + 0x9E3779B9) & 0xFFFFFFFF)
+    jx, jy = np.float32(h1 >> 8) * np.float32(2.0 ** -24), np.float32(h2 >> 8) * np.float32(2.0 ** -24)
+    assert 0 <= jx < 1 and 0 <= jy < 1
