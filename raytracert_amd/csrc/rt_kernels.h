@@ -38,6 +38,21 @@ struct ShadeParams {
     float pad;
 };
 
+// Where a shadow kernel's queries come from (isShadow, raytracing.cpp:241-261). Compacted: the
+// shadow queue k_shadow_gen wrote (sq_org/sq_dst, count). Virtual: query j is pair (j / L, j % L)
+// of the step's main queue, read straight from its hits (origin hit_I + 0.1, destination the
+// light); pairs whose query missed are inactive and the kernel counts the active ones into
+// pair_count (the shadow-ray statistic k_shadow_gen's compaction would have produced).
+struct ShadowSource {
+    const float4 *sq_org, *sq_dst;
+    const int32_t *count;           // compacted: queue size; virtual: the main queue's size
+    const int32_t *hit_idx;
+    const float4 *hit_I;
+    int32_t *pair_count;
+    int32_t n_lights, virt;
+    float lights[RT_MAX_LIGHTS][3];
+};
+
 // Device views of one scene and one render workspace.
 struct DevScene {
     const TriRec *tris;
@@ -90,7 +105,8 @@ void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream
 void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevWork &w, hipStream_t stream);
 void launch_closest_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream);
 void launch_shadow_gen(const DevScene &s, const DevWork &w, const ShadeParams &p, int64_t capacity, hipStream_t stream);
-void launch_shadow_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream);
+void launch_shadow_hit(const DevScene &s, const DevWork &w, const ShadeParams &p, bool virt, int64_t capacity,
+                       hipStream_t stream);
 void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int64_t capacity, hipStream_t stream);
 void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream);
 void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t stream);

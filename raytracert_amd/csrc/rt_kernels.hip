@@ -330,11 +330,23 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
         test_triangle<kAnyHit, true>(T, t, o, dir, best, bidx, bI, done);
     }
     if (!active || (kAnyHit && done)) return;
-    RayBox R;
-    R.o = o;
-    R.inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
-    R.pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
-    R.dlen = sqrtf(dot(dir, dir));
+    // Per-ray constants. inv is clamped to |inv| <= 2^100 (dir components of 0 or below 2^-100):
+    // with the scene below 1e6 in magnitude (dev_view falls back to the binary tree otherwise)
+    // no slab distance can be NaN, and a clamped axis only narrows a slab where no hit can exist
+    // (|n.dir| >= 1e-5 needs |dir| >= 2.5e-18 there). Near and far planes are chosen once by the
+    // sign of inv, so each bound costs one byte convert and one fma.
+    V3 inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+    constexpr float kInvMax = 0x1p100f;
+    if (!(fabsf(inv.x) <= kInvMax)) inv.x = copysignf(kInvMax, dir.x);
+    if (!(fabsf(inv.y) <= kInvMax)) inv.y = copysignf(kInvMax, dir.y);
+    if (!(fabsf(inv.z) <= kInvMax)) inv.z = copysignf(kInvMax, dir.z);
+    const float pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
+    const float dlen = sqrtf(dot(dir, dir));
+    const bool nx = inv.x < 0, ny = inv.y < 0, nz = inv.z < 0;
+    const float pnx = nx ? pad : -pad, pny = ny ? pad : -pad, pnz = nz ? pad : -pad;   // near plane = lo - pad / hi + pad
+    // distance cull: a child whose entry exceeds tcull cannot hold an accepted point nearer than
+    // best ((t dlen - pad)(1 - 1e-5) > best, with slack for this bound's own rounding)
+    float tcull = INFINITY;
     int sp = 0;
     int32_t ref = 0;
     while (true) {
@@ -342,28 +354,29 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
             ++visits;
             const uint4 *np = reinterpret_cast<const uint4 *>(sc.nodes4 + ref);
             const uint4 a = np[0], b = np[1], c = np[2], d = np[3];
-            const float ox = __uint_as_float(a.x), oy = __uint_as_float(a.y), oz = __uint_as_float(a.z);
-            const float sx = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w)) + 127) << 23);
-            const float sy = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 8)) + 127) << 23);
-            const float sz = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 16)) + 127) << 23);
+            const float dx = __uint_as_float(a.x) - o.x, dy = __uint_as_float(a.y) - o.y, dz = __uint_as_float(a.z) - o.z;
+            const float kx = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w)) + 127) << 23) * inv.x;
+            const float ky = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 8)) + 127) << 23) * inv.y;
+            const float kz = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 16)) + 127) << 23) * inv.z;
+            const float cnx = (dx + pnx) * inv.x, cfx = (dx - pnx) * inv.x;
+            const float cny = (dy + pny) * inv.y, cfy = (dy - pny) * inv.y;
+            const float cnz = (dz + pnz) * inv.z, cfz = (dz - pnz) * inv.z;
+            const uint32_t wnx = nx ? b.w : b.x, wfx = nx ? b.x : b.w;   // qlo / qhi words per axis
+            const uint32_t wny = ny ? c.x : b.y, wfy = ny ? b.y : c.x;
+            const uint32_t wnz = nz ? c.y : b.z, wfz = nz ? b.z : c.y;
             int32_t rc[4] = {static_cast<int32_t>(c.z), static_cast<int32_t>(c.w), static_cast<int32_t>(d.x),
                              static_cast<int32_t>(d.y)};
-            // The ray origin and pad are folded into the node frame once: a bound's slab distance is
-            // fma(q, scale, origin -/+ pad - o) * inv, the same rounding budget as box_hit's
-            // (bound - pad - o) * inv (bvh.cpp: both are far inside the pad's margin).
-            const float lx = (ox - R.pad) - R.o.x, ly = (oy - R.pad) - R.o.y, lz = (oz - R.pad) - R.o.z;
-            const float hx = (ox + R.pad) - R.o.x, hy = (oy + R.pad) - R.o.y, hz = (oz + R.pad) - R.o.z;
             float tc[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const float ax = q_decode(lx, sx, b.x, k) * R.inv.x, bx = q_decode(hx, sx, b.w, k) * R.inv.x;
-                const float ay = q_decode(ly, sy, b.y, k) * R.inv.y, by = q_decode(hy, sy, c.x, k) * R.inv.y;
-                const float az = q_decode(lz, sz, b.z, k) * R.inv.z, bz = q_decode(hz, sz, c.y, k) * R.inv.z;
-                const float te = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
-                const float tx = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                const float tnx = q_decode(cnx, kx, wnx, k), tfx = q_decode(cfx, kx, wfx, k);
+                const float tny = q_decode(cny, ky, wny, k), tfy = q_decode(cfy, ky, wfy, k);
+                const float tnz = q_decode(cnz, kz, wnz, k), tfz = q_decode(cfz, kz, wfz, k);
+                const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
+                const float tx = fminf(fminf(tfx, tfy), tfz);
                 bool h = te <= tx * 1.00001f;
                 h = h && rc[k] != kBvhEmpty;
-                if (!kAnyHit) h = h && (te * R.dlen - R.pad) * 0.99999f <= best;
+                if (!kAnyHit) h = h && te <= tcull;
                 tc[k] = h ? fminf(te, FLT_MAX) : INFINITY;   // hits sort before misses
             }
             cswap(tc[0], rc[0], tc[1], rc[1]);
@@ -385,6 +398,7 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
             const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
             const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
             test_leaf<kAnyHit>(sc, first, cnt, o, dir, best, bidx, bI, done);
+            if (!kAnyHit && best < FLT_MAX) tcull = (best * 1.00002f + pad) / dlen * 1.00001f;
             tests += static_cast<unsigned>(cnt);
             if (kAnyHit && done) break;
             if (sp == 0) break;
@@ -541,24 +555,55 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_closest_hit(const DevScene sc
     wt.flush(sc.work);
 }
 
+// Shadow query j of a ShadowSource: ray and output slot; false if the pair is inactive.
+__device__ __forceinline__ bool shadow_query(const ShadowSource &src, int j, int end, V3 &o, V3 &dir, int &slot) {
+    if (j >= end) return false;
+    if (src.virt) {
+        const int L = src.n_lights;
+        const int k = j / L, l = j - k * L;
+        if (src.hit_idx[k] < 0) return false;
+        const float4 I = src.hit_I[k];
+        o = mk(I.x + 0.1f, I.y + 0.1f, I.z + 0.1f);                                    // :248
+        dir = mk(src.lights[l][0] - o.x, src.lights[l][1] - o.y, src.lights[l][2] - o.z);
+        slot = j;
+        return true;
+    }
+    const float4 qo = src.sq_org[j], qd = src.sq_dst[j];
+    o = mk(qo.x, qo.y, qo.z);
+    dir = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);
+    slot = as_int(qo.w);
+    return true;
+}
+
+__device__ __forceinline__ int shadow_total(const ShadowSource &src) {
+    return src.virt ? *src.count * src.n_lights : *src.count;
+}
+
+// Virtual sources: the block's active pairs, one atomic per block (ray statistics).
+__device__ __forceinline__ void add_pair_count(const ShadowSource &src, unsigned mine) {
+    if (!src.virt) return;
+    __shared__ unsigned s_pairs;
+    if (threadIdx.x == 0) s_pairs = 0;
+    __syncthreads();
+    unsigned long long c = mine;
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    if (__lane_id() == 0 && c) atomicAdd(&s_pairs, static_cast<unsigned>(c));
+    __syncthreads();
+    if (threadIdx.x == 0 && s_pairs) atomicAdd(src.pair_count, static_cast<int32_t>(s_pairs));
+}
+
 template <bool kAnyHit, int W, bool kCount>
-__global__ __launch_bounds__(kBvhBlock) void k_bvh_shadow_hit(const DevScene sc, const float4 *__restrict__ q_org,
-                                                              const float4 *__restrict__ q_dst,
-                                                              const int32_t *__restrict__ q_count,
+__global__ __launch_bounds__(kBvhBlock) void k_bvh_shadow_hit(const DevScene sc, const ShadowSource src,
                                                               uint8_t *__restrict__ shadow, int32_t *__restrict__ wq) {
     extern __shared__ int32_t lds_stack[];
     const LaneStack stack = lane_stack(sc, lds_stack);
     WorkTally<kCount> wt;
-    drive_queries(*q_count, sc.xcd_split, wq, [&](int j, int end) {
-        const bool active = j < end;
+    unsigned pairs = 0;
+    drive_queries(shadow_total(src), sc.xcd_split, wq, [&](int j, int end) {
         V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
         int slot = 0;
-        if (active) {
-            const float4 qo = q_org[j], qd = q_dst[j];
-            o = mk(qo.x, qo.y, qo.z);
-            dir = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);
-            slot = as_int(qo.w);
-        }
+        const bool active = shadow_query(src, j, end, o, dir, slot);
+        pairs += active;
         int bidx = -1;
         V3 bI = mk(0, 0, 0);
         wt.begin();
@@ -566,11 +611,12 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_shadow_hit(const DevScene sc,
         wt.end();
         if (active) {
             uint8_t sh = 0;
-            if (bidx >= 0) sh = sc.mats[sc.tri_mat[bidx]].transparent ? 0 : 1;
+            if (bidx >= 0) sh = sc.mats[sc.tri_mat[bidx]].transparent ? 0 : 1;   // :253-257
             shadow[slot] = sh;
         }
     });
     wt.flush(sc.work ? sc.work + kWorkFields : nullptr);
+    add_pair_count(src, pairs);
 }
 
 template <int W, bool kCount>
@@ -630,32 +676,24 @@ __global__ __launch_bounds__(kBlock) void k_closest_hit(const TriRec *__restrict
 template <bool kAnyHit>
 __global__ __launch_bounds__(kBlock) void k_shadow_hit(const TriRec *__restrict__ tris, int nt,
                                                        const uint32_t *__restrict__ tri_mat,
-                                                       const DevMaterial *__restrict__ mats,
-                                                       const float4 *__restrict__ q_org,
-                                                       const float4 *__restrict__ q_dst,
-                                                       const int32_t *__restrict__ q_count,
+                                                       const DevMaterial *__restrict__ mats, const ShadowSource src,
                                                        uint8_t *__restrict__ shadow) {
-    const int n = *q_count;
+    const int n = shadow_total(src);
     const int base = blockIdx.x * kBlock;
     if (base >= n) return;
     const int j = base + threadIdx.x;
-    const bool active = j < n;
     V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
     int slot = 0;
-    if (active) {
-        const float4 qo = q_org[j], qd = q_dst[j];
-        o = mk(qo.x, qo.y, qo.z);
-        dir = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);
-        slot = as_int(qo.w);
-    }
+    const bool active = shadow_query(src, j, n, o, dir, slot);
     int bidx = -1;
     V3 bI = mk(0, 0, 0);
-    closest_hit_loop<kAnyHit>(tris, nt, o, dir, active, bidx, bI);
+    if (__any(active)) closest_hit_loop<kAnyHit>(tris, nt, o, dir, active, bidx, bI);
     if (active) {
         uint8_t sh = 0;
         if (bidx >= 0) sh = mats[tri_mat[bidx]].transparent ? 0 : 1;               // :253-257
         shadow[slot] = sh;
     }
+    add_pair_count(src, active ? 1u : 0u);
 }
 
 __global__ __launch_bounds__(kBlock) void k_intersect_only(const TriRec *__restrict__ tris, int nt,
@@ -1066,25 +1104,37 @@ void launch_shadow_gen(const DevScene &, const DevWork &w, const ShadeParams &p,
     hipLaunchKernelGGL(k_shadow_gen, dim3(grid_chunked(n)), dim3(kBlock), 0, stream, p, w);
 }
 
-void launch_shadow_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
+void launch_shadow_hit(const DevScene &s, const DevWork &w, const ShadeParams &p, bool virt, int64_t capacity,
+                       hipStream_t stream) {
     if (capacity <= 0) return;
+    const int step = p.step;
+    ShadowSource src{};
+    src.sq_org = w.sq_org;
+    src.sq_dst = w.sq_dst;
+    src.count = virt ? &w.counters[step] : &w.counters[kMaxStepsCounters + step];
+    src.hit_idx = w.hit_idx;
+    src.hit_I = w.hit_I;
+    src.pair_count = &w.counters[kMaxStepsCounters + step];
+    src.n_lights = p.n_lights;
+    src.virt = virt ? 1 : 0;
+    for (int l = 0; l < RT_MAX_LIGHTS; ++l)
+        for (int k = 0; k < 3; ++k) src.lights[l][k] = p.lights[l][k];
     if (s.use_bvh) {
         auto k = s.bvh_width == 4 ? (s.any_transparent ? k_bvh_shadow_hit<false, 4, false> : k_bvh_shadow_hit<true, 4, false>)
                                   : (s.any_transparent ? k_bvh_shadow_hit<false, 2, false> : k_bvh_shadow_hit<true, 2, false>);
         if (s.work)
             k = s.bvh_width == 4 ? (s.any_transparent ? k_bvh_shadow_hit<false, 4, true> : k_bvh_shadow_hit<true, 4, true>)
                                  : (s.any_transparent ? k_bvh_shadow_hit<false, 2, true> : k_bvh_shadow_hit<true, 2, true>);
-        hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s,
-                           w.sq_org, w.sq_dst, &w.counters[kMaxStepsCounters + step], w.shadow,
+        hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, src, w.shadow,
                            w.wq + (2 * step + 1) * kWqSlot);
         return;
     }
     if (s.any_transparent)
-        hipLaunchKernelGGL(k_shadow_hit<false>, dim3(grid_for(capacity)), dim3(kBlock), 0, stream, s.tris, s.nt,
-                           s.tri_mat, s.mats, w.sq_org, w.sq_dst, &w.counters[kMaxStepsCounters + step], w.shadow);
+        hipLaunchKernelGGL(k_shadow_hit<false>, dim3(grid_for(capacity)), dim3(kBlock), 0, stream, s.tris, s.nt, s.tri_mat,
+                           s.mats, src, w.shadow);
     else
-        hipLaunchKernelGGL(k_shadow_hit<true>, dim3(grid_for(capacity)), dim3(kBlock), 0, stream, s.tris, s.nt,
-                           s.tri_mat, s.mats, w.sq_org, w.sq_dst, &w.counters[kMaxStepsCounters + step], w.shadow);
+        hipLaunchKernelGGL(k_shadow_hit<true>, dim3(grid_for(capacity)), dim3(kBlock), 0, stream, s.tris, s.nt, s.tri_mat,
+                           s.mats, src, w.shadow);
 }
 
 void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int64_t capacity, hipStream_t stream) {

@@ -275,11 +275,14 @@ def test_multi_frame_shard_batch_reassembles(workdir, gpu_available):
                                    {"xcd_split": 2, "bvh_grid": 3}, {"xcd_split": 1, "bvh_grid": 5},
                                    {"bvh_width": 2, "xcd_split": 2}, {"lds_stack": 1}, {"lds_stack": 5, "bvh_grid": 7},
                                    {"bvh_width": 2, "lds_stack": 2}, {"pipes": 1}, {"pipes": 3},
-                                   {"pipes": 4, "xcd_split": 2}])
+                                   {"pipes": 4, "xcd_split": 2}, {"shadow_virtual": 0}, {"shadow_virtual": 5},
+                                   {"shadow_virtual": 0, "bvh_width": 2}])
 def test_launch_shape_knobs_never_change_results(knobs, workdir, gpu_available):
     """Query distribution (grid-stride, static XCD segments, work-stealing XCD queues), tiny grids
     (fewer blocks than XCDs), tree width and the LDS/HBM split of the traversal stack (1 entry in
-    LDS: nearly every push overflows) are placement choices only: byte-identical frames."""
+    LDS: nearly every push overflows), render pipelines and whether shadow rays come from a
+    compacted queue or straight from the hits are placement choices only: byte-identical frames
+    and ray counts."""
     p = R.RenderParams(width=320, height=180, pf=2, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
     with R.Scene.load(scene_path("syn:C4", workdir), device=0) as sc:
         ref, reff, refc = sc.render(p, want_f32=True)
