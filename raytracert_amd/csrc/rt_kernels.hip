@@ -233,62 +233,16 @@ __device__ __forceinline__ bool box_hit(const RayBox &R, float lx, float ly, flo
     return tmin <= tmax * 1.00001f;
 }
 
-// rayIntersectTriangle + the lexicographic update for a tree triangle (D finite and nonzero: the
-// builder sends every other triangle to the always list). Same result as test_triangle; the
-// three divisions are skipped whenever their outcome is already decided exactly:
-//  * r < 0 (:125) iff a != 0 and a, b have opposite signs (b finite, |b| >= 1e-5);
-//  * closest-hit: no accepted point can be nearer than |r| |dir| less the rounding of I, so a
-//    candidate with |a / b| |dir| (1 - 1e-5) > best + pad is never accepted (pad = the per-ray
-//    64 eps (|o|_1 + M_1) >> the 2 eps |o| rounding of I; the approximate quotient is within a
-//    few ulp);
-//  * s < 0 / t < 0 iff the finite numerator and D have opposite signs; s > 1 and s + t > 1 are
-//    certain once the approximate quotients exceed 1 by 2e-6 / 4e-6 (far above their ulp error).
-// Everything that survives runs the reference's divisions and tests unchanged.
-template <bool kAnyHit>
-__device__ __forceinline__ void test_triangle_tree(const TriRec &T, int t, V3 o, V3 dir, float pad, float dlen,
-                                                   float &best, int &bidx, V3 &bI, bool &done) {
-    if (kAnyHit && done) return;
-    const V3 w0 = mk(o.x - T.t0[0], o.y - T.t0[1], o.z - T.t0[2]);
-    const float b = T.n[0] * dir.x + T.n[1] * dir.y + T.n[2] * dir.z;          // :113
-    const float a = -(T.n[0] * w0.x + T.n[1] * w0.y + T.n[2] * w0.z);          // :114
-    if (fabsf(b) < 0.00001f) return;                                            // :115
-    if (fabsf(b) <= FLT_MAX && a != 0.0f && ((a < 0.0f) != (b < 0.0f))) return;  // r < 0 (:125)
-    if (!kAnyHit && fabsf(a * __builtin_amdgcn_rcpf(b)) * dlen * 0.99999f > best + pad) return;
-    const float r = a / b;                                                      // :124
-    if (r < 0) return;                                                          // :125
-    const V3 I = mk(o.x + dir.x * r, o.y + dir.y * r, o.z + dir.z * r);         // :130
-    const V3 w = mk(I.x - T.t0[0], I.y - T.t0[1], I.z - T.t0[2]);               // :137
-    const float wu = w.x * T.u[0] + w.y * T.u[1] + w.z * T.u[2];                 // :138
-    const float wv = w.x * T.v[0] + w.y * T.v[1] + w.z * T.v[2];                 // :139
-    const float sn = T.uv * wv - T.vv * wu, tn = T.uv * wu - T.uu * wv;         // :144, :148 numerators
-    if (fabsf(sn) <= FLT_MAX && fabsf(tn) <= FLT_MAX) {
-        const bool dneg = T.D < 0.0f;
-        if (sn != 0.0f && ((sn < 0.0f) != dneg)) return;                         // s < 0
-        if (tn != 0.0f && ((tn < 0.0f) != dneg)) return;                         // t < 0
-        const float rd = __builtin_amdgcn_rcpf(T.D);
-        const float sa = sn * rd, ta = tn * rd;
-        if (sa > 1.000002f || sa + ta > 1.000004f) return;                      // s > 1, s + t > 1
-    }
-    const float s = sn / T.D;                                                   // :144
-    if (s < 0 || s > 1) return;                                                 // :145
-    const float tt = tn / T.D;                                                  // :148
-    if (tt < 0 || (s + tt) > 1) return;                                         // :149
-    const V3 e = sub(o, I);                                                     // distance, Vec3D.h:199-202
-    const float dist = sqrtf(dot(e, e));
-    if (dist < best || (dist == best && t < bidx)) {                            // lexicographic (dist, index)
-        best = dist; bidx = t; bI = I;
-        if (kAnyHit) done = true;
-    }
-}
-
 // A leaf's records in leaf order. The original index (ties, result) is read only when a test
 // reaches the comparison with the current best.
+// (Skipping the divisions when their outcome is decided by signs or approximate quotients was
+// measured slower: the extra branches and registers cost more than the divisions they save.)
 template <bool kAnyHit>
-__device__ __forceinline__ void test_leaf(const DevScene &sc, int first, int cnt, V3 o, V3 dir, float pad, float dlen,
-                                          float &best, int &bidx, V3 &bI, bool &done) {
+__device__ __forceinline__ void test_leaf(const DevScene &sc, int first, int cnt, V3 o, V3 dir, float &best, int &bidx,
+                                          V3 &bI, bool &done) {
     for (int k = 0; k < cnt; ++k) {
         const TriRec T = sc.leaf_recs[first + k];
-        test_triangle_tree<kAnyHit>(T, static_cast<int>(sc.leaf_idx[first + k]), o, dir, pad, dlen, best, bidx, bI, done);
+        test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first + k]), o, dir, best, bidx, bI, done);
     }
 }
 
@@ -340,7 +294,7 @@ __device__ __forceinline__ void bvh_query(const DevScene &sc, V3 o, V3 dir, bool
             const uint32_t u = static_cast<uint32_t>(ref);
             const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
             const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
-            test_leaf<kAnyHit>(sc, first, cnt, o, dir, R.pad, R.dlen, best, bidx, bI, done);
+            test_leaf<kAnyHit>(sc, first, cnt, o, dir, best, bidx, bI, done);
             tests += static_cast<unsigned>(cnt);
             if (kAnyHit && done) break;
             if (sp == 0) break;
@@ -444,7 +398,7 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
             const uint32_t u = static_cast<uint32_t>(ref);
             const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
             const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
-            test_leaf<kAnyHit>(sc, first, cnt, o, dir, pad, dlen, best, bidx, bI, done);
+            test_leaf<kAnyHit>(sc, first, cnt, o, dir, best, bidx, bI, done);
             if (!kAnyHit && best < FLT_MAX) tcull = (best * 1.00002f + pad) / dlen * 1.00001f;
             tests += static_cast<unsigned>(cnt);
             if (kAnyHit && done) break;
