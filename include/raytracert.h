@@ -203,6 +203,10 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
 #define RT_TUNE_BVH_WIDTH 2   /* 4 (default): quantised four-wide nodes; 2: float binary nodes */
 #define RT_TUNE_LDS_STACK 3   /* traversal stack entries per lane kept in LDS; deeper ones in HBM */
 #define RT_TUNE_PIPES     4   /* 1-4 render pipelines (workspace + stream) a call's batches overlap on */
+#define RT_TUNE_WAVE_TRAVERSAL 8   /* bit k: closest-hit of chain step k, bit 16+k: its shadow rays,
+                                      bit 31: rt_intersect_mesh, walk the four-wide tree once per
+                                      wave (coherent rays); default 0: measured no faster on C4,
+                                      primaries included (VALU-bound, not fetch-bound) */
 #define RT_TUNE_PIPE_BATCHES 6     /* split a call into at least pipes x this many batches */
 #define RT_TUNE_PIPE_PRIORITY 7    /* 1 (default): pipelines after the first run at lower stream priority */
 #define RT_TUNE_SHADOW_VIRTUAL 5   /* bit k: step k's shadow rays are read from its hits directly

@@ -73,6 +73,8 @@ struct DevScene {
     int32_t bvh_width;              // 2 or 4 (RT_TUNE_BVH_WIDTH)
     int32_t bvh4_stack;             // four-wide stack entries needed (3 per inner level)
     int32_t lds_stack;              // stack entries per lane held in LDS (<= entries needed)
+    int32_t wave_mask;              // RT_TUNE_WAVE_TRAVERSAL: bit k closest-hit step k, bit 16+k shadow step k,
+                                    // bit 31 rt_intersect_mesh use the wave-coherent four-wide kernel
     int32_t *stack_ovf;             // deeper entries: [entry - lds_stack][grid lane], grid <= bvh_grid
     int32_t xcd_split;              // RT_TUNE_XCD_SPLIT
     int32_t bvh_grid;               // RT_TUNE_BVH_GRID

@@ -408,10 +408,129 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Wave-coherent four-wide traversal (W = 5): the 64 lanes of a wave walk ONE path through the
+// tree. A node's child is visited when any lane's box test (same arithmetic as bvh4_query) wants
+// it, so every lane still visits every node its own traversal would and tests a superset of its
+// triangles; the lexicographic minimum is order-independent, so results are identical. What it
+// buys for coherent rays (a tile's primaries, their shadow rays): node and triangle records are
+// wave-uniform, fetched by scalar loads into SGPRs instead of 64 vector loads of the same bytes,
+// the stack is one wave-uniform LDS column, and there is no per-lane divergence in the loop.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int32_t uniform(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+template <bool kAnyHit>
+__device__ __forceinline__ void wave_query(const DevScene &sc, const Bvh4Node *__restrict__ nodes,
+                                           const TriRec *__restrict__ recs, const uint32_t *__restrict__ ridx, V3 o,
+                                           V3 dir, bool active, int &bidx, V3 &bI, int32_t *wstack, unsigned &tests,
+                                           unsigned &visits) {
+    float best = FLT_MAX;
+    bool done = !active;
+    for (int i = 0; i < sc.n_always; ++i) {
+        const int t = static_cast<int>(sc.always[i]);
+        const TriRec T = sc.tris[t];
+        test_triangle<kAnyHit, true>(T, t, o, dir, best, bidx, bI, done);
+    }
+    if (!__any(!done)) return;
+    V3 inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+    constexpr float kInvMax = 0x1p100f;   // see bvh4_query
+    if (!(fabsf(inv.x) <= kInvMax)) inv.x = copysignf(kInvMax, dir.x);
+    if (!(fabsf(inv.y) <= kInvMax)) inv.y = copysignf(kInvMax, dir.y);
+    if (!(fabsf(inv.z) <= kInvMax)) inv.z = copysignf(kInvMax, dir.z);
+    const float pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
+    const float dlen = sqrtf(dot(dir, dir));
+    const bool nx = inv.x < 0, ny = inv.y < 0, nz = inv.z < 0;
+    const float pnx = nx ? pad : -pad, pny = ny ? pad : -pad, pnz = nz ? pad : -pad;
+    float tcull = done ? -INFINITY : INFINITY;   // a finished lane wants no child
+    int sp = 0;
+    int32_t ref = 0;
+    while (true) {
+        if (ref >= 0) {
+            ++visits;
+            const Bvh4Node &nd = nodes[ref];
+            const uint32_t aw = static_cast<uint32_t>(static_cast<uint8_t>(nd.ex[0])) |
+                                (static_cast<uint32_t>(static_cast<uint8_t>(nd.ex[1])) << 8) |
+                                (static_cast<uint32_t>(static_cast<uint8_t>(nd.ex[2])) << 16);
+            const float dx = nd.origin[0] - o.x, dy = nd.origin[1] - o.y, dz = nd.origin[2] - o.z;
+            const float kx = __int_as_float((static_cast<int>(static_cast<int8_t>(aw)) + 127) << 23) * inv.x;
+            const float ky = __int_as_float((static_cast<int>(static_cast<int8_t>(aw >> 8)) + 127) << 23) * inv.y;
+            const float kz = __int_as_float((static_cast<int>(static_cast<int8_t>(aw >> 16)) + 127) << 23) * inv.z;
+            const float cnx = (dx + pnx) * inv.x, cfx = (dx - pnx) * inv.x;
+            const float cny = (dy + pny) * inv.y, cfy = (dy - pny) * inv.y;
+            const float cnz = (dz + pnz) * inv.z, cfz = (dz - pnz) * inv.z;
+            const uint32_t wnx = nx ? nd.qhi[0] : nd.qlo[0], wfx = nx ? nd.qlo[0] : nd.qhi[0];
+            const uint32_t wny = ny ? nd.qhi[1] : nd.qlo[1], wfy = ny ? nd.qlo[1] : nd.qhi[1];
+            const uint32_t wnz = nz ? nd.qhi[2] : nd.qlo[2], wfz = nz ? nd.qlo[2] : nd.qhi[2];
+            float key[4];
+            int32_t rc[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float tnx = q_decode(cnx, kx, wnx, k), tfx = q_decode(cfx, kx, wfx, k);
+                const float tny = q_decode(cny, ky, wny, k), tfy = q_decode(cfy, ky, wfy, k);
+                const float tnz = q_decode(cnz, kz, wnz, k), tfz = q_decode(cfz, kz, wfz, k);
+                const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
+                const float tx = fminf(fminf(tfx, tfy), tfz);
+                const bool h = te <= tx * 1.00001f && te <= tcull;
+                const unsigned long long m = __ballot(h);
+                rc[k] = nd.child[k];
+                // the wave's order key: the entry distance of the first lane that wants the child
+                key[k] = (m && rc[k] != kBvhEmpty)
+                             ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fminf(te, FLT_MAX)),
+                                                                        __ffsll(static_cast<long long>(m)) - 1))
+                             : INFINITY;
+            }
+            cswap(key[0], rc[0], key[1], rc[1]);
+            cswap(key[2], rc[2], key[3], rc[3]);
+            cswap(key[0], rc[0], key[2], rc[2]);
+            cswap(key[1], rc[1], key[3], rc[3]);
+            cswap(key[1], rc[1], key[2], rc[2]);
+            if (key[3] != INFINITY) { if (__lane_id() == 0) wstack[sp] = rc[3]; ++sp; }
+            if (key[2] != INFINITY) { if (__lane_id() == 0) wstack[sp] = rc[2]; ++sp; }
+            if (key[1] != INFINITY) { if (__lane_id() == 0) wstack[sp] = rc[1]; ++sp; }
+            if (key[0] != INFINITY) {
+                ref = uniform(rc[0]);
+            } else {
+                if (sp == 0) break;
+                ref = uniform(wstack[--sp]);
+            }
+        } else {
+            const uint32_t u = static_cast<uint32_t>(ref);
+            const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
+            const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
+            for (int k = 0; k < cnt; ++k) {
+                const TriRec T = recs[first + k];
+                if (!done) test_triangle<kAnyHit, true>(T, static_cast<int>(ridx[first + k]), o, dir, best, bidx, bI, done);
+            }
+            tests += static_cast<unsigned>(cnt);
+            if (kAnyHit) {
+                if (done) tcull = -INFINITY;
+                if (!__any(!done)) break;
+            } else if (best < FLT_MAX) {
+                tcull = (best * 1.00002f + pad) / dlen * 1.00001f;
+            }
+            if (sp == 0) break;
+            ref = uniform(wstack[--sp]);
+        }
+    }
+}
+
+// Scalar-loadable views of the four-wide tree (kernel arguments marked __restrict__, so the
+// compiler may fetch wave-uniform records with s_load).
+struct TreeArgs {
+    const Bvh4Node *nodes;
+    const TriRec *recs;
+    const uint32_t *idx;
+};
+
 template <bool kAnyHit, int W>
-__device__ __forceinline__ void bvh_query_w(const DevScene &sc, V3 o, V3 dir, bool active, int &bidx, V3 &bI,
+__device__ __forceinline__ void bvh_query_w(const DevScene &sc, const Bvh4Node *__restrict__ n4,
+                                            const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx,
+                                            int32_t *lds, V3 o, V3 dir, bool active, int &bidx, V3 &bI,
                                             const LaneStack &stack, unsigned &tests, unsigned &visits) {
-    if (W == 4) bvh4_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
+    if (W == 5) wave_query<kAnyHit>(sc, n4, lrec, lidx, o, dir, active, bidx, bI, lds + (threadIdx.x >> 6) * sc.bvh4_stack,
+                                    tests, visits);
+    else if (W == 4) bvh4_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
     else bvh_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
 }
 
@@ -530,7 +649,9 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_closest_hit(const DevScene sc
                                                                const float4 *__restrict__ q_dst,
                                                                const int32_t *__restrict__ q_count,
                                                                int32_t *__restrict__ hit_idx, float4 *__restrict__ hit_I,
-                                                               int32_t *__restrict__ wq) {
+                                                               int32_t *__restrict__ wq, const Bvh4Node *__restrict__ n4,
+                                                               const TriRec *__restrict__ lrec,
+                                                               const uint32_t *__restrict__ lidx) {
     extern __shared__ int32_t lds_stack[];
     const LaneStack stack = lane_stack(sc, lds_stack);
     WorkTally<kCount> wt;
@@ -546,7 +667,7 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_closest_hit(const DevScene sc
         int bidx = -1;
         V3 bI = mk(0, 0, 0);
         wt.begin();
-        bvh_query_w<false, W>(sc, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
+        bvh_query_w<false, W>(sc, n4, lrec, lidx, lds_stack, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
         wt.end();
         if (j < end) {
             hit_idx[j] = bidx;
@@ -595,7 +716,9 @@ __device__ __forceinline__ void add_pair_count(const ShadowSource &src, unsigned
 
 template <bool kAnyHit, int W, bool kCount>
 __global__ __launch_bounds__(kBvhBlock) void k_bvh_shadow_hit(const DevScene sc, const ShadowSource src,
-                                                              uint8_t *__restrict__ shadow, int32_t *__restrict__ wq) {
+                                                              uint8_t *__restrict__ shadow, int32_t *__restrict__ wq,
+                                                              const Bvh4Node *__restrict__ n4, const TriRec *__restrict__ lrec,
+                                                              const uint32_t *__restrict__ lidx) {
     extern __shared__ int32_t lds_stack[];
     const LaneStack stack = lane_stack(sc, lds_stack);
     WorkTally<kCount> wt;
@@ -608,7 +731,7 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_shadow_hit(const DevScene sc,
         int bidx = -1;
         V3 bI = mk(0, 0, 0);
         wt.begin();
-        bvh_query_w<kAnyHit, W>(sc, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
+        bvh_query_w<kAnyHit, W>(sc, n4, lrec, lidx, lds_stack, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
         wt.end();
         if (active) {
             uint8_t sh = 0;
@@ -623,7 +746,10 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_shadow_hit(const DevScene sc,
 template <int W, bool kCount>
 __global__ __launch_bounds__(kBvhBlock) void k_bvh_intersect_only(const DevScene sc, const float4 *__restrict__ q_org,
                                                                   const float4 *__restrict__ q_dst, int n,
-                                                                  int32_t *__restrict__ idx, float4 *__restrict__ I) {
+                                                                  int32_t *__restrict__ idx, float4 *__restrict__ I,
+                                                                  const Bvh4Node *__restrict__ n4,
+                                                                  const TriRec *__restrict__ lrec,
+                                                                  const uint32_t *__restrict__ lidx) {
     extern __shared__ int32_t lds_stack[];
     const LaneStack stack = lane_stack(sc, lds_stack);
     WorkTally<kCount> wt;
@@ -638,7 +764,7 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_intersect_only(const DevScene
         int bidx = -1;
         V3 bI = mk(0, 0, 0);
         wt.begin();
-        bvh_query_w<false, W>(sc, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
+        bvh_query_w<false, W>(sc, n4, lrec, lidx, lds_stack, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
         wt.end();
         if (active) { idx[j] = bidx; I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f); }
     });
@@ -1085,14 +1211,31 @@ inline unsigned grid_stride(int64_t n) {
     return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, kMaxGrid)));
 }
 
+// Tree kernel variant: 2 (binary, per lane), 4 (four-wide, per lane) or 5 (four-wide,
+// wave-coherent; DevScene::wave_mask bit `bit`).
+inline int tree_variant(const DevScene &s, int bit) {
+    if (s.bvh_width != 4) return 2;
+    return (bit >= 0 && ((static_cast<uint32_t>(s.wave_mask) >> bit) & 1u)) ? 5 : 4;
+}
+inline size_t tree_lds(const DevScene &s, int W) {
+    return W == 5 ? sizeof(int32_t) * (kBvhBlock / kWave) * static_cast<size_t>(std::max(s.bvh4_stack, 1)) : bvh_lds(s);
+}
+
+template <int W>
+void launch_ch(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
+    auto k = s.work ? k_bvh_closest_hit<W, true> : k_bvh_closest_hit<W, false>;
+    hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), tree_lds(s, W), stream, s,
+                       w.q_org[step & 1], w.q_dst[step & 1], &w.counters[step], w.hit_idx, w.hit_I,
+                       w.wq + (2 * step) * kWqSlot, s.nodes4, s.leaf_recs, s.leaf_idx);
+}
+
 void launch_closest_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
     if (capacity <= 0) return;
     if (s.use_bvh) {
-        auto k = s.work ? (s.bvh_width == 4 ? k_bvh_closest_hit<4, true> : k_bvh_closest_hit<2, true>)
-                        : (s.bvh_width == 4 ? k_bvh_closest_hit<4, false> : k_bvh_closest_hit<2, false>);
-        hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s,
-                           w.q_org[step & 1], w.q_dst[step & 1], &w.counters[step], w.hit_idx, w.hit_I,
-                           w.wq + (2 * step) * kWqSlot);
+        const int W = tree_variant(s, std::min(step, 15));
+        if (W == 5) launch_ch<5>(s, w, step, capacity, stream);
+        else if (W == 4) launch_ch<4>(s, w, step, capacity, stream);
+        else launch_ch<2>(s, w, step, capacity, stream);
         return;
     }
     hipLaunchKernelGGL(k_closest_hit, dim3(grid_for(capacity)), dim3(kBlock), 0, stream, s.tris, s.nt,
@@ -1103,6 +1246,15 @@ void launch_shadow_gen(const DevScene &, const DevWork &w, const ShadeParams &p,
     const int64_t n = capacity * p.n_lights;
     if (n <= 0) return;
     hipLaunchKernelGGL(k_shadow_gen, dim3(grid_chunked(n)), dim3(kBlock), 0, stream, p, w);
+}
+
+template <int W>
+void launch_sh(const DevScene &s, const DevWork &w, const ShadowSource &src, int step, int64_t capacity,
+               hipStream_t stream) {
+    auto k = s.any_transparent ? k_bvh_shadow_hit<false, W, false> : k_bvh_shadow_hit<true, W, false>;
+    if (s.work) k = s.any_transparent ? k_bvh_shadow_hit<false, W, true> : k_bvh_shadow_hit<true, W, true>;
+    hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), tree_lds(s, W), stream, s, src, w.shadow,
+                       w.wq + (2 * step + 1) * kWqSlot, s.nodes4, s.leaf_recs, s.leaf_idx);
 }
 
 void launch_shadow_hit(const DevScene &s, const DevWork &w, const ShadeParams &p, bool virt, int64_t capacity,
@@ -1121,13 +1273,10 @@ void launch_shadow_hit(const DevScene &s, const DevWork &w, const ShadeParams &p
     for (int l = 0; l < RT_MAX_LIGHTS; ++l)
         for (int k = 0; k < 3; ++k) src.lights[l][k] = p.lights[l][k];
     if (s.use_bvh) {
-        auto k = s.bvh_width == 4 ? (s.any_transparent ? k_bvh_shadow_hit<false, 4, false> : k_bvh_shadow_hit<true, 4, false>)
-                                  : (s.any_transparent ? k_bvh_shadow_hit<false, 2, false> : k_bvh_shadow_hit<true, 2, false>);
-        if (s.work)
-            k = s.bvh_width == 4 ? (s.any_transparent ? k_bvh_shadow_hit<false, 4, true> : k_bvh_shadow_hit<true, 4, true>)
-                                 : (s.any_transparent ? k_bvh_shadow_hit<false, 2, true> : k_bvh_shadow_hit<true, 2, true>);
-        hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, src, w.shadow,
-                           w.wq + (2 * step + 1) * kWqSlot);
+        const int W = tree_variant(s, 16 + std::min(step, 15));
+        if (W == 5) launch_sh<5>(s, w, src, step, capacity, stream);
+        else if (W == 4) launch_sh<4>(s, w, src, step, capacity, stream);
+        else launch_sh<2>(s, w, src, step, capacity, stream);
         return;
     }
     if (s.any_transparent)
@@ -1159,9 +1308,12 @@ void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *d
                            float4 *I, hipStream_t stream) {
     if (n <= 0) return;
     if (s.use_bvh) {
-        auto k = s.work ? (s.bvh_width == 4 ? k_bvh_intersect_only<4, true> : k_bvh_intersect_only<2, true>)
-                        : (s.bvh_width == 4 ? k_bvh_intersect_only<4, false> : k_bvh_intersect_only<2, false>);
-        hipLaunchKernelGGL(k, dim3(grid_bvh(n, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, org, dst, n, idx, I);
+        const int W = tree_variant(s, 31);
+        auto k = W == 5 ? (s.work ? k_bvh_intersect_only<5, true> : k_bvh_intersect_only<5, false>)
+                 : W == 4 ? (s.work ? k_bvh_intersect_only<4, true> : k_bvh_intersect_only<4, false>)
+                          : (s.work ? k_bvh_intersect_only<2, true> : k_bvh_intersect_only<2, false>);
+        hipLaunchKernelGGL(k, dim3(grid_bvh(n, s.bvh_grid)), dim3(kBvhBlock), tree_lds(s, W), stream, s, org, dst, n, idx, I,
+                           s.nodes4, s.leaf_recs, s.leaf_idx);
         return;
     }
     hipLaunchKernelGGL(k_intersect_only, dim3(grid_for(n)), dim3(kBlock), 0, stream, s.tris, s.nt, org, dst, n, idx, I);

@@ -192,7 +192,7 @@ def _query_mix(sc, rng, n):
     return o, d
 
 
-@pytest.mark.parametrize("width", [2, 4])
+@pytest.mark.parametrize("width", [2, 4, 5])
 @pytest.mark.parametrize("spec", ["ref:dodgeColorTest.obj", "ref:Models/shadow_test.obj", "syn:F4", "syn:C4"])
 def test_bvh_matches_brute_force_bitwise(spec, width, workdir, gpu_available):
     path = scene_path(spec, workdir)
@@ -202,7 +202,8 @@ def test_bvh_matches_brute_force_bitwise(spec, width, workdir, gpu_available):
         sc.set_accel("brute_force")
         bi, bp = sc.intersect_mesh(o, d)
         sc.set_accel("bvh")
-        sc.tune("bvh_width", width)
+        sc.tune("bvh_width", min(width, 4))
+        sc.tune("wave_traversal", -1 if width == 5 else 0)   # 5: the wave-coherent four-wide kernel
         assert sc.accel() == "bvh"
         vi, vp = sc.intersect_mesh(o, d)
     assert np.array_equal(bi, vi), np.nonzero(bi != vi)[0][:10]
@@ -276,7 +277,9 @@ def test_multi_frame_shard_batch_reassembles(workdir, gpu_available):
                                    {"bvh_width": 2, "xcd_split": 2}, {"lds_stack": 1}, {"lds_stack": 5, "bvh_grid": 7},
                                    {"bvh_width": 2, "lds_stack": 2}, {"pipes": 1}, {"pipes": 3},
                                    {"pipes": 4, "xcd_split": 2}, {"shadow_virtual": 0}, {"shadow_virtual": 5},
-                                   {"shadow_virtual": 0, "bvh_width": 2}])
+                                   {"shadow_virtual": 0, "bvh_width": 2}, {"wave_traversal": 0},
+                                   {"wave_traversal": -1}, {"wave_traversal": -1, "shadow_virtual": 0},
+                                   {"wave_traversal": -1, "lds_stack": 1}])
 def test_launch_shape_knobs_never_change_results(knobs, workdir, gpu_available):
     """Query distribution (grid-stride, static XCD segments, work-stealing XCD queues), tiny grids
     (fewer blocks than XCDs), tree width and the LDS/HBM split of the traversal stack (1 entry in
