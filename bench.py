@@ -47,6 +47,11 @@ WORKLOADS = {
                     "the reference's regular AA grid), depth 3, 4 lights",
                scene="syn:C5", width=3840, height=2160, pf=2, max_lvl=3,
                lights=((0.0, 0.0, 4.0), (1.5, 1.5, 4.0), (-1.5, 1.5, 4.0), (0.0, -1.5, 4.0))),
+    "c5s": dict(desc="C5 stochastic: synthetic 16x16 UV-sphere grid OBJ (1,015,810 tris) 3840x2160, 4 jittered "
+                     "samples/pixel (RT_STOCHASTIC, seed 0x5EED: pf 2 strata, counter-hash jitter; an extension of "
+                     "the reference's regular grid), depth 3, 4 lights",
+                scene="syn:C5", width=3840, height=2160, pf=2, max_lvl=3, stochastic=True,
+                lights=((0.0, 0.0, 4.0), (1.5, 1.5, 4.0), (-1.5, 1.5, 4.0), (0.0, -1.5, 4.0))),
 }
 
 
@@ -121,7 +126,8 @@ def main():
     t_load = time.time() - t_load
     bvh_info = scene.bvh_info() if args.accel == "bvh" else None
     nv, nt, nm = scene.counts()
-    params = R.RenderParams(width=WIDTH, height=HEIGHT, pf=PF, max_lvl=MAX_LVL, lights=LIGHTS)
+    flags = R.ALL_FEATURES | (R._capi.STOCHASTIC if wl.get("stochastic") else 0)
+    params = R.RenderParams(width=WIDTH, height=HEIGHT, pf=PF, max_lvl=MAX_LVL, lights=LIGHTS, flags=flags)
     cparams = params.to_c()
 
     layout = rdist.TileLayout(WIDTH, HEIGHT, TILE, TILE)
@@ -335,9 +341,12 @@ def pmc_traffic(kernel: str):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        k = d.get("kernels", {}).get(kernel)
-        if k and "traffic_bytes_per_launch" in k:
-            return k["traffic_bytes_per_launch"], os.path.relpath(f, HERE)
+        ks = d.get("kernels", {})
+        # the timed (non-counting) instantiation of the kernel, e.g. "k_bvh_closest_hit<4, false>"
+        names = [n for n in ks if n == kernel or (n.startswith(kernel + "<") and n.endswith("false>"))]
+        for n in names:
+            if "traffic_bytes_per_launch" in ks[n]:
+                return ks[n]["traffic_bytes_per_launch"], os.path.relpath(f, HERE)
     return None, None
 
 
@@ -348,7 +357,8 @@ def cpu_baseline(obj, params, gpu_frame, layout, args, wl):
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     import oracle as O
     sc = O.OracleScene(obj)
-    op = O.make_params(params.width, params.height, params.pf, params.max_lvl, lights=params.lights)
+    op = O.make_params(params.width, params.height, params.pf, params.max_lvl, lights=params.lights, flags=params.flags,
+                       seed=params.seed)
     tiles = list(range(0, layout.n_tiles, args.cpu_sample_every))
     threads = args.cpu_threads
     rays = 0
