@@ -66,6 +66,7 @@ struct DevScene {
     const TriRec *leaf_recs;
     const uint32_t *leaf_idx;
     const uint32_t *always;
+    const TriRec *always_recs;      // the always list's records, contiguous
     int32_t use_bvh, n_always;
     float scene_m1;
     int32_t bvh_depth;              // traversal stack entries needed (tree depth)

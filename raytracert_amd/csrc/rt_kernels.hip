@@ -233,6 +233,32 @@ __device__ __forceinline__ bool box_hit(const RayBox &R, float lx, float ly, flo
     return tmin <= tmax * 1.00001f;
 }
 
+// The always list (ill-conditioned triangles, bvh.cpp): every query tests them. Their records are
+// gathered contiguously (always_recs) and streamed like the brute-force loop: wave-uniform,
+// two records alternating so one load is in flight behind the arithmetic.
+template <bool kAnyHit>
+__device__ __forceinline__ void test_always(const DevScene &sc, V3 o, V3 dir, float &best, int &bidx, V3 &bI,
+                                            bool &done) {
+    const int n = sc.n_always;
+    if (n <= 0) return;
+    const TriRec *__restrict__ recs = sc.always_recs;
+    TriRec A = recs[0];
+    int i = 0;
+    for (; i + 1 < n; i += 2) {
+        if (kAnyHit && (i & 15) == 0 && __all(done)) return;
+        sgpr_fence(A);
+        const TriRec B = recs[i + 1];
+        test_triangle<kAnyHit, true>(A, static_cast<int>(sc.always[i]), o, dir, best, bidx, bI, done);
+        sgpr_fence(B);
+        A = recs[min(i + 2, n - 1)];
+        test_triangle<kAnyHit, true>(B, static_cast<int>(sc.always[i + 1]), o, dir, best, bidx, bI, done);
+    }
+    if (i < n) {
+        sgpr_fence(A);
+        test_triangle<kAnyHit, true>(A, static_cast<int>(sc.always[i]), o, dir, best, bidx, bI, done);
+    }
+}
+
 // A leaf's records in leaf order. The original index (ties, result) is read only when a test
 // reaches the comparison with the current best.
 // (Skipping the divisions when their outcome is decided by signs or approximate quotients was
@@ -251,12 +277,7 @@ __device__ __forceinline__ void bvh_query(const DevScene &sc, V3 o, V3 dir, bool
                                           const LaneStack &stack, unsigned &tests, unsigned &visits) {
     float best = FLT_MAX;
     bool done = !active;
-    // ill-conditioned triangles: every query, in index order (wave-uniform scalar loads)
-    for (int i = 0; i < sc.n_always; ++i) {
-        const int t = static_cast<int>(sc.always[i]);
-        const TriRec T = sc.tris[t];
-        test_triangle<kAnyHit, true>(T, t, o, dir, best, bidx, bI, done);
-    }
+    test_always<kAnyHit>(sc, o, dir, best, bidx, bI, done);
     if (!active || (kAnyHit && done)) return;
     RayBox R;
     R.o = o;
@@ -325,11 +346,7 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
                                            const LaneStack &stack, unsigned &tests, unsigned &visits) {
     float best = FLT_MAX;
     bool done = !active;
-    for (int i = 0; i < sc.n_always; ++i) {
-        const int t = static_cast<int>(sc.always[i]);
-        const TriRec T = sc.tris[t];
-        test_triangle<kAnyHit, true>(T, t, o, dir, best, bidx, bI, done);
-    }
+    test_always<kAnyHit>(sc, o, dir, best, bidx, bI, done);
     if (!active || (kAnyHit && done)) return;
     // Per-ray constants. inv is clamped to |inv| <= 2^100 (dir components of 0 or below 2^-100):
     // with the scene below 1e6 in magnitude (dev_view falls back to the binary tree otherwise)
@@ -427,11 +444,7 @@ __device__ __forceinline__ void wave_query(const DevScene &sc, const Bvh4Node *_
                                            unsigned &visits) {
     float best = FLT_MAX;
     bool done = !active;
-    for (int i = 0; i < sc.n_always; ++i) {
-        const int t = static_cast<int>(sc.always[i]);
-        const TriRec T = sc.tris[t];
-        test_triangle<kAnyHit, true>(T, t, o, dir, best, bidx, bI, done);
-    }
+    test_always<kAnyHit>(sc, o, dir, best, bidx, bI, done);
     if (!__any(!done)) return;
     V3 inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
     constexpr float kInvMax = 0x1p100f;   // see bvh4_query
