@@ -22,7 +22,8 @@
 //    pad_ray = 64 eps (|o|_1 + M_1) to every box at traversal time (M_1 = max |x|+|y|+|z| of the
 //    vertices), which also covers the rounding of I itself.
 //  * Triangles with D == 0 or non-finite (then s, t are NaN/inf and the reference accepts almost
-//    anything), or with K eps > 0.05 (angle at T0 below ~1.6 degrees), are not put in the tree:
+//    anything), or with K eps > 0.2 (angle at T0 below ~1 degree; there the first-order bound's
+//    second-order terms, ~(K eps)^2, stay far inside the factor-4 pad), are not put in the tree:
 //    every query tests them first (the "always" list). Triangles with n == 0 are rejected by
 //    isNullVector and never tested.
 //  * Box tests and the distance cull use relative slack (1e-5) far above their rounding error.
@@ -47,7 +48,7 @@ namespace rt {
 namespace {
 
 constexpr double kEps = 5.9604644775390625e-08;   // 2^-24
-constexpr double kMaxDelta = 0.05;   // K*eps bound for a tree triangle (pad <= 0.42 L)
+constexpr double kMaxDelta = 0.2;    // K*eps bound for a tree triangle (pad <= 2 L): angle at T0 >~ 1 degree
 constexpr int kBins = 16;
 constexpr int kMaxLeaf = 4;
 

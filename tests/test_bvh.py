@@ -117,7 +117,7 @@ def test_bvh_structure(spec, workdir):
     assert 1 <= info["depth"] <= 40
     assert 1 <= info["depth4"] <= info["depth"] and 1 <= info["nodes4"] <= max(info["nodes"], 1)
     if nt > 1000:
-        assert info["always"] < nt * 0.02   # dodgeColorTest: 184 slivers with < 1.6 degrees at T0
+        assert info["always"] < nt * 0.005   # dodgeColorTest: 30 slivers with < ~1 degree at T0
 
 
 def test_bvh_on_tiny_and_degenerate_scenes(tmp_path):
@@ -169,3 +169,25 @@ def test_parallel_build_is_the_sequential_tree(workdir, monkeypatch):
         digests[t] = s.bvh_digest()
         s.bvh_validate()
     assert len(set(digests.values())) == 1, digests
+
+
+def test_acceptance_claim_on_near_threshold_slivers():
+    """Slivers whose angle at T0 puts K eps between 0.02 and 0.2 (the tree's upper limit, ~1 to
+    2 degrees): the largest pads the tree uses. Many rays aimed at the edges and vertices, grazing
+    and from far away, against the oracle's arithmetic."""
+    rng = np.random.default_rng(23)
+    n_box = 0
+    accepted = 0
+    for i in range(40):
+        theta = np.deg2rad(rng.uniform(0.95, 2.2))
+        L = 10 ** rng.uniform(-2, 2)
+        base = rng.normal(size=3) * 10 ** rng.uniform(-1, 2)
+        e1 = rng.normal(size=3); e1 /= np.linalg.norm(e1)
+        e2 = rng.normal(size=3); e2 -= (e2 @ e1) * e1; e2 /= np.linalg.norm(e2)
+        la, lb = L, L * rng.uniform(0.3, 1.0)
+        T = np.stack([base, base + la * e1, base + lb * (np.cos(theta) * e1 + np.sin(theta) * e2)]).astype(np.float32)
+        for far in (False, True):
+            st, n = _check_triangle(T, _rays_near(T, rng, 6000, far=far))
+            n_box += st == 0
+            accepted += n
+    assert n_box >= 60 and accepted > 3000
