@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c4")
     ap.add_argument("--no-bf-roofline", action="store_true", help="skip the brute-force kernel's roofline frame")
     ap.add_argument("--pipes", type=int, default=2, help="render pipelines a call's batches overlap on")
+    ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
+                    help="extra launch-shape knob (Scene.tune), e.g. shadow_virtual=-1; repeatable")
     return ap.parse_args()
 
 
@@ -123,6 +125,9 @@ def main():
     scene = R.Scene.load(obj, device=local_rank)
     scene.set_accel(args.accel)
     scene.tune("pipes", args.pipes)
+    for kv in args.tune:
+        k, v = kv.split("=", 1)
+        scene.tune(k, int(v, 0))
     t_load = time.time() - t_load
     bvh_info = scene.bvh_info() if args.accel == "bvh" else None
     nv, nt, nm = scene.counts()
