@@ -1,10 +1,10 @@
 // rt_kernels.hip — gfx950 kernels of the render path.
 //
-// Wavefront structure (one launch per stage, queues compacted with wave-aggregated atomics):
+// Wavefront structure (one launch per stage, queues compacted with one atomic per block chunk):
 //   gen_primary  -> main queue Q0 (one query per sub-sample; main.cpp:369-388)
 //   per chain step k = 0..max_lvl:
 //     closest_hit(Q_k)            intersectMesh, raytracing.cpp:161-192   <- the hot kernel
-//     shadow_gen + shadow_hit     isShadow, raytracing.cpp:241-261 (any-hit when no material is
+//     [shadow_gen +] shadow_hit   isShadow, raytracing.cpp:241-261 (any-hit when no material is
 //                                 transparent, closest-hit + material test otherwise)
 //     shade(Q_k) -> Q_{k+1}       shade/diffuse/specular/reflection/refraction, :194-368
 //   frame        fold the chain back to front (trace() returns are consumed innermost first),
@@ -961,32 +961,6 @@ __global__ __launch_bounds__(kBlock) void k_shadow_gen(const ShadeParams p, DevW
     }
 }
 
-// Compacts the secondary rays k_shade left densely in sq_org/sq_dst (lvl < 0 = none) into the
-// next step's queue, in order.
-__global__ __launch_bounds__(kBlock) void k_compact_next(const ShadeParams p, DevWork w) {
-    const int total = w.counters[p.step];
-    const int nb = (p.step + 1) & 1;
-    for (int base = blockIdx.x * kBlock * kPer; base < total; base += gridDim.x * kBlock * kPer) {
-        bool valid[kPer];
-        int pos[kPer];
-        float4 d[kPer];
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const int j = base + k * kBlock + threadIdx.x;
-            d[k] = j < total ? w.sq_dst[j] : make_float4(0, 0, 0, as_float(-1));
-            valid[k] = as_int(d[k].w) >= 0;
-        }
-        block_reserve_rounds<kBlock, kPer>(valid, &w.counters[p.step + 1], pos);
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            if (!valid[k]) continue;
-            const int j = base + k * kBlock + threadIdx.x;
-            w.q_org[nb][pos[k]] = w.sq_org[j];
-            w.q_dst[nb][pos[k]] = d[k];
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------------------------
 // shade (raytracing.cpp:335-368) for one hit, plus the secondary ray it spawns.
 // ---------------------------------------------------------------------------------------------
@@ -1016,19 +990,23 @@ __device__ __forceinline__ void offset_point(V3 &point, V3 dest) {   // addOffse
     point = add(point, v);
 }
 
-// One lane per query, grid-stride over the step's queue. The secondary ray (if any) is written
-// densely at the query's position in sq_org/sq_dst (lvl -1 = none; the shadow queue is consumed
-// by then) and compacted into the next queue by k_compact_next.
-__global__ __launch_bounds__(kBlock) void k_shade(const DevScene sc, const ShadeParams p, DevWork w) {
+// One thread per query of the step's queue; the secondary rays go straight into the next
+// step's queue, compacted with one atomic per 1,024-query block round (a single counter word
+// takes only ~88 atomics/us, so per-wave appends are too slow).
+constexpr int kShadeBlock = 1024;
+__global__ __launch_bounds__(kShadeBlock) void k_shade(const DevScene sc, const ShadeParams p, DevWork w) {
     const int n = w.counters[p.step];
-    for (int j = blockIdx.x * kBlock + threadIdx.x; j < n; j += gridDim.x * kBlock) {
+    const int nb = (p.step + 1) & 1;
+    for (int base = blockIdx.x * kShadeBlock; base < n; base += gridDim.x * kShadeBlock) {   // uniform per block
+    const int j = base + static_cast<int>(threadIdx.x);
     Secondary sec;
     sec.state = kChildNone;
     sec.org = mk(0, 0, 0);
     sec.dst = mk(0, 0, 0);
     sec.lvl = -1;
     int sample = 0;
-    const float4 qo = w.q_org[p.step & 1][j], qd = w.q_dst[p.step & 1][j];
+    const float4 qo = j < n ? w.q_org[p.step & 1][j] : make_float4(0, 0, 0, 0);
+    const float4 qd = j < n ? w.q_dst[p.step & 1][j] : make_float4(0, 0, 0, as_float(-1));
     const int lvl = as_int(qd.w);
     if (lvl >= 0) {                                                       // inactive (outside frame) otherwise
         sample = as_int(qo.w);
@@ -1128,9 +1106,13 @@ __global__ __launch_bounds__(kBlock) void k_shade(const DevScene sc, const Shade
             else w.depth[sample] = static_cast<uint8_t>(p.step + 1);
         }
     }
-    const bool spawn = sec.state == kChildTrace;
-    w.sq_org[j] = make_float4(sec.org.x, sec.org.y, sec.org.z, as_float(sample));
-    w.sq_dst[j] = make_float4(sec.dst.x, sec.dst.y, sec.dst.z, as_float(spawn ? sec.lvl : -1));
+    bool spawn[1] = {sec.state == kChildTrace};
+    int pos[1];
+    block_reserve_rounds<kShadeBlock, 1>(spawn, &w.counters[p.step + 1], pos);
+    if (spawn[0]) {
+        w.q_org[nb][pos[0]] = make_float4(sec.org.x, sec.org.y, sec.org.z, as_float(sample));
+        w.q_dst[nb][pos[0]] = make_float4(sec.dst.x, sec.dst.y, sec.dst.z, as_float(sec.lvl));
+    }
     }
 }
 
@@ -1304,8 +1286,8 @@ void launch_shadow_hit(const DevScene &s, const DevWork &w, const ShadeParams &p
 
 void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int64_t capacity, hipStream_t stream) {
     if (capacity <= 0) return;
-    hipLaunchKernelGGL(k_shade, dim3(grid_stride(capacity)), dim3(kBlock), 0, stream, s, p, w);
-    hipLaunchKernelGGL(k_compact_next, dim3(grid_chunked(capacity)), dim3(kBlock), 0, stream, p, w);
+    const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((capacity + kShadeBlock - 1) / kShadeBlock, 1024)));
+    hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kShadeBlock), 0, stream, s, p, w);
 }
 
 void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream) {
