@@ -293,6 +293,14 @@ bool make_node4(const Box *boxes, const int32_t *refs, int nc, Bvh4Node &g) {
         if (nc == 0) continue;
         if (!quantize_axis(u.lo[k], u.hi[k], boxes, nc, k, g)) return false;
     }
+    // empty slots get an inverted box (lo byte 255, hi byte 0 on every axis): the slab test
+    // rejects it whatever the ray's direction (and if rounding ever let one through, its ref is an
+    // empty leaf, which tests nothing), so the kernel needs no per-child empty check
+    for (int c = nc; c < 4; ++c)
+        for (int k = 0; k < 3; ++k) {
+            g.qlo[k] |= 0xFFu << (8 * c);
+            g.qhi[k] &= ~(0xFFu << (8 * c));
+        }
     return true;
 }
 

@@ -399,16 +399,24 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
                 const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
                 const float tx = fminf(fminf(tfx, tfy), tfz);
                 bool h = te <= tx * 1.00001f;
-                h = h && rc[k] != kBvhEmpty;
                 if (!kAnyHit) h = h && te <= tcull;
                 tc[k] = h ? fminf(te, FLT_MAX) : INFINITY;   // hits sort before misses
             }
             if (!kAnyHit || kSortAnyHit) {
+                // (the network costs ~25 VALU; nodes where one child or none is wanted skip it)
+                const int nh = (tc[0] != INFINITY) + (tc[1] != INFINITY) + (tc[2] != INFINITY) + (tc[3] != INFINITY);
+                if (nh > 1) {
                 cswap(tc[0], rc[0], tc[1], rc[1]);
                 cswap(tc[2], rc[2], tc[3], rc[3]);
                 cswap(tc[0], rc[0], tc[2], rc[2]);
                 cswap(tc[1], rc[1], tc[3], rc[3]);
                 cswap(tc[1], rc[1], tc[2], rc[2]);
+                } else if (nh == 1) {   // bring the one wanted child to the front
+                    const int32_t one = tc[0] != INFINITY ? rc[0] : tc[1] != INFINITY ? rc[1] : tc[2] != INFINITY ? rc[2] : rc[3];
+                    rc[0] = one;
+                    tc[0] = 0.0f;
+                    tc[1] = tc[2] = tc[3] = INFINITY;
+                }
                 if (tc[3] != INFINITY) stack.push(sp, rc[3]);
                 if (tc[2] != INFINITY) stack.push(sp, rc[2]);
                 if (tc[1] != INFINITY) stack.push(sp, rc[1]);
