@@ -32,7 +32,7 @@ HAS_KD, HAS_KA, HAS_KS, HAS_NS, HAS_NI, HAS_TR, HAS_ILLUM = (1 << i for i in ran
 KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME = range(4)
 ACCEL_BRUTE_FORCE, ACCEL_BVH = 0, 1
 TUNE_XCD_SPLIT, TUNE_BVH_GRID, TUNE_BVH_WIDTH, TUNE_LDS_STACK, TUNE_PIPES, TUNE_SHADOW_VIRTUAL = 0, 1, 2, 3, 4, 5
-TUNE_PIPE_BATCHES, TUNE_PIPE_PRIORITY, TUNE_WAVE_TRAVERSAL = 6, 7, 8
+TUNE_PIPE_BATCHES, TUNE_PIPE_PRIORITY, TUNE_WAVE_TRAVERSAL, TUNE_CHAIN_FROM = 6, 7, 8, 9
 BVH_INFO_FIELDS = 7
 STOCHASTIC = 1 << 8
 DEFAULT_SEED = 0x5EED

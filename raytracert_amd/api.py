@@ -237,13 +237,13 @@ class Scene:
 
     def tune(self, knob: str, value: int) -> None:
         """Launch-shape knobs ('xcd_split', 'bvh_grid', 'bvh_width', 'lds_stack', 'pipes',
-        'shadow_virtual', 'pipe_batches', 'pipe_priority', 'wave_traversal'); outputs never depend
-        on them."""
+        'shadow_virtual', 'pipe_batches', 'pipe_priority', 'wave_traversal', 'chain_from'); outputs
+        never depend on them."""
         k = {"xcd_split": _capi.TUNE_XCD_SPLIT, "bvh_grid": _capi.TUNE_BVH_GRID,
              "bvh_width": _capi.TUNE_BVH_WIDTH, "lds_stack": _capi.TUNE_LDS_STACK,
              "pipes": _capi.TUNE_PIPES, "shadow_virtual": _capi.TUNE_SHADOW_VIRTUAL,
              "pipe_batches": _capi.TUNE_PIPE_BATCHES, "pipe_priority": _capi.TUNE_PIPE_PRIORITY,
-             "wave_traversal": _capi.TUNE_WAVE_TRAVERSAL}[knob]
+             "wave_traversal": _capi.TUNE_WAVE_TRAVERSAL, "chain_from": _capi.TUNE_CHAIN_FROM}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
 
     def bvh_digest(self) -> int:

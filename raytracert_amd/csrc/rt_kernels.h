@@ -112,6 +112,9 @@ void launch_shadow_hit(const DevScene &s, const DevWork &w, const ShadeParams &p
                        hipStream_t stream);
 void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int64_t capacity, hipStream_t stream);
 void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream);
+// Steps first..max_lvl of every query in Q_first in one launch (closest-hit, shadows, shade per lane).
+void launch_chain(const DevScene &s, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
+                  hipStream_t stream);
 void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t stream);
 void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *dst, int32_t n,
                            int32_t *idx, float4 *I, hipStream_t stream);

@@ -1024,126 +1024,205 @@ __device__ __forceinline__ void offset_point(V3 &point, V3 dest) {   // addOffse
 // One thread per query of the step's queue; the secondary rays go straight into the next
 // step's queue, compacted with one atomic per 1,024-query block round (a single counter word
 // takes only ~88 atomics/us, so per-wave appends are too slow).
-constexpr int kShadeBlock = 1024;
-__global__ __launch_bounds__(kShadeBlock) void k_shade(const DevScene sc, const ShadeParams p, DevWork w) {
-    const int n = w.counters[p.step];
-    const int nb = (p.step + 1) & 1;
-    for (int base = blockIdx.x * kShadeBlock; base < n; base += gridDim.x * kShadeBlock) {   // uniform per block
-    const int j = base + static_cast<int>(threadIdx.x);
+// shade (raytracing.cpp:335-368) for a hit of the chain step `step`: writes the step's chain
+// record (local colour and child state, the child's coefficient, the depth when the chain ends)
+// and returns the secondary ray, if any. is_shadowed(l) is isShadow's verdict for light l.
+template <typename Shadowed>
+__device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadeParams &p, const DevWork &w, int step,
+                                               int sample, V3 origin, V3 dest, int lvl, int idx, V3 P,
+                                               Shadowed &&is_shadowed) {
     Secondary sec;
     sec.state = kChildNone;
     sec.org = mk(0, 0, 0);
     sec.dst = mk(0, 0, 0);
     sec.lvl = -1;
-    int sample = 0;
-    const float4 qo = j < n ? w.q_org[p.step & 1][j] : make_float4(0, 0, 0, 0);
-    const float4 qd = j < n ? w.q_dst[p.step & 1][j] : make_float4(0, 0, 0, as_float(-1));
-    const int lvl = as_int(qd.w);
-    if (lvl >= 0) {                                                       // inactive (outside frame) otherwise
-        sample = as_int(qo.w);
-        int idx = w.hit_idx[j];
-        if (idx >= sc.nt) {                       // never expected: flag it for the host, do not fault
-            w.counters[kErrorSlot] = 1;
-            idx = -1;
+    const int64_t ci = static_cast<int64_t>(step) * w.cap + sample;
+    const V3 ray = sub(dest, origin);                                // :393
+    V3 normal = ld3(sc.normals[idx]);                                // :394 (copy, mutated below)
+    const DevMaterial m = sc.mats[sc.tri_mat[idx]];                  // :396
+    const V3 Kd = mk(m.Kd[0], m.Kd[1], m.Kd[2]);
+    const V3 Ka = mk(m.Ka[0], m.Ka[1], m.Ka[2]);
+    const V3 Ks = mk(m.Ks[0], m.Ks[1], m.Ks[2]);
+    const uint32_t f = p.flags;
+    V3 color = mk(0, 0, 0);                                          // :336
+    if ((f & RT_AMBIENT) && (m.flags & RT_HAS_KA)) color = add(color, Ka);   // :337-340
+    for (int l = 0; l < p.n_lights; ++l) {                           // :342
+        const V3 L = mk(p.lights[l][0], p.lights[l][1], p.lights[l][2]);
+        const bool shadowed = (f & RT_SHADOWS) ? is_shadowed(l) : false;
+        if (shadowed) continue;
+        if ((f & RT_DIFFUSE) && (m.flags & RT_HAS_KD)) {             // diffuseOnly :197-205
+            V3 diffuse = mk(0, 0, 0);
+            normalize(normal);
+            V3 lp = L;
+            normalize(lp);
+            diffuse = add(diffuse, scale(Kd, max_std(dot(normal, lp), 0.0f)));
+            color = add(color, scale(diffuse, m.Tr));                // :349
         }
-        const int64_t ci = static_cast<int64_t>(p.step) * w.cap + sample;
-        if (idx < 0) {                                                   // trace() miss -> BLACK (:389-391)
-            w.chain_local[ci] = make_float4(0, 0, 0, as_float(kChildNone));
-            w.depth[sample] = static_cast<uint8_t>(p.step + 1);
+        if ((f & RT_SPECULAR) && (m.flags & RT_HAS_KS) && (m.flags & RT_HAS_NS)) {   // :210-232
+            V3 spec = mk(0, 0, 0);
+            V3 Vv = sub(mk(p.cam[0], p.cam[1], p.cam[2]), P);
+            normalize(normal);
+            normalize(Vv);
+            V3 Lv = sub(L, P);
+            normalize(Lv);
+            V3 H = add(Vv, Lv);
+            normalize(H);
+            float st = max_std(dot(H, normal), 0.0f);
+            st = spec_powf(st, m.Ns);
+            spec = add(spec, scale(Ks, st));
+            color = add(color, scale(spec, m.Tr));                   // :353
+        }
+    }
+    if ((f & RT_REFRACTION) && (m.Tr < 1) && lvl < p.max_lvl) {     // :357-359 -> refraction :290-330
+        const int rl = lvl + 1;
+        V3 r = ray;
+        normalize(r);
+        const float check = dot(r, normal);
+        sec.state = kChildZero;
+        if (check < 0) {
+            if (check >= kAcosLe2Threshold) {                        // 0 < acosf(check) <= 2
+                sec.state = kChildTrace; sec.coef = Ks; sec.lvl = rl + 1;
+                reflection_ray(r, P, normal, sec.org, sec.dst);
+            } else {
+                const float nr = 1 / m.Ni;
+                const float root = 1 - m.powf_nr2 * (1 - glibc_powf2(dot(normal, r), sc.ties, sc.n_ties));
+                if (root >= 0.0f) {
+                    const float rt = sqrtf(root);
+                    const V3 T = sub(scale(sub(r, scale(normal, dot(normal, r))), nr), scale(normal, rt));
+                    sec.org = P;
+                    sec.dst = add(P, T);
+                    offset_point(sec.org, sec.dst);
+                    sec.state = kChildTrace; sec.lvl = rl + 1;
+                    const float c = 1 - m.Tr;
+                    sec.coef = mk(c, c, c);
+                }
+            }
         } else {
-            const V3 origin = mk(qo.x, qo.y, qo.z), dest = mk(qd.x, qd.y, qd.z);
-            const V3 ray = sub(dest, origin);                                // :393
-            V3 normal = ld3(sc.normals[idx]);                                // :394 (copy, mutated below)
-            const DevMaterial m = sc.mats[sc.tri_mat[idx]];                  // :396
-            const V3 P = ld3(w.hit_I[j]);
-            const V3 Kd = mk(m.Kd[0], m.Kd[1], m.Kd[2]);
-            const V3 Ka = mk(m.Ka[0], m.Ka[1], m.Ka[2]);
-            const V3 Ks = mk(m.Ks[0], m.Ks[1], m.Ks[2]);
-            const uint32_t f = p.flags;
-            V3 color = mk(0, 0, 0);                                          // :336
-            if ((f & RT_AMBIENT) && (m.flags & RT_HAS_KA)) color = add(color, Ka);   // :337-340
-            for (int l = 0; l < p.n_lights; ++l) {                           // :342
-                const V3 L = mk(p.lights[l][0], p.lights[l][1], p.lights[l][2]);
-                const bool shadowed = (f & RT_SHADOWS) ? (w.shadow[j * p.n_lights + l] != 0) : false;
-                if (shadowed) continue;
-                if ((f & RT_DIFFUSE) && (m.flags & RT_HAS_KD)) {             // diffuseOnly :197-205
-                    V3 diffuse = mk(0, 0, 0);
-                    normalize(normal);
-                    V3 lp = L;
-                    normalize(lp);
-                    diffuse = add(diffuse, scale(Kd, max_std(dot(normal, lp), 0.0f)));
-                    color = add(color, scale(diffuse, m.Tr));                // :349
-                }
-                if ((f & RT_SPECULAR) && (m.flags & RT_HAS_KS) && (m.flags & RT_HAS_NS)) {   // :210-232
-                    V3 spec = mk(0, 0, 0);
-                    V3 Vv = sub(mk(p.cam[0], p.cam[1], p.cam[2]), P);
-                    normalize(normal);
-                    normalize(Vv);
-                    V3 Lv = sub(L, P);
-                    normalize(Lv);
-                    V3 H = add(Vv, Lv);
-                    normalize(H);
-                    float st = max_std(dot(H, normal), 0.0f);
-                    st = spec_powf(st, m.Ns);
-                    spec = add(spec, scale(Ks, st));
-                    color = add(color, scale(spec, m.Tr));                   // :353
-                }
+            const float nr = m.Ni;
+            const V3 nn = neg(normal);
+            const float root = 1 - m.powf_ni2 * (1 - glibc_powf2(dot(nn, r), sc.ties, sc.n_ties));
+            if (root >= 0.0f) {
+                const float rt = sqrtf(root);
+                const V3 T = sub(scale(sub(r, scale(nn, dot(nn, r))), nr), scale(nn, rt));
+                sec.org = P;
+                sec.dst = add(P, T);
+                offset_point(sec.org, sec.dst);
+                sec.state = kChildTrace; sec.lvl = rl + 1;
+                const float c = 1 - m.Tr;
+                sec.coef = mk(c, c, c);
             }
-            if ((f & RT_REFRACTION) && (m.Tr < 1) && lvl < p.max_lvl) {     // :357-359 -> refraction :290-330
-                const int rl = lvl + 1;
-                V3 r = ray;
-                normalize(r);
-                const float check = dot(r, normal);
-                sec.state = kChildZero;
-                if (check < 0) {
-                    if (check >= kAcosLe2Threshold) {                        // 0 < acosf(check) <= 2
-                        sec.state = kChildTrace; sec.coef = Ks; sec.lvl = rl + 1;
-                        reflection_ray(r, P, normal, sec.org, sec.dst);
-                    } else {
-                        const float nr = 1 / m.Ni;
-                        const float root = 1 - m.powf_nr2 * (1 - glibc_powf2(dot(normal, r), sc.ties, sc.n_ties));
-                        if (root >= 0.0f) {
-                            const float rt = sqrtf(root);
-                            const V3 T = sub(scale(sub(r, scale(normal, dot(normal, r))), nr), scale(normal, rt));
-                            sec.org = P;
-                            sec.dst = add(P, T);
-                            offset_point(sec.org, sec.dst);
-                            sec.state = kChildTrace; sec.lvl = rl + 1;
-                            const float c = 1 - m.Tr;
-                            sec.coef = mk(c, c, c);
-                        }
-                    }
-                } else {
-                    const float nr = m.Ni;
-                    const V3 nn = neg(normal);
-                    const float root = 1 - m.powf_ni2 * (1 - glibc_powf2(dot(nn, r), sc.ties, sc.n_ties));
-                    if (root >= 0.0f) {
-                        const float rt = sqrtf(root);
-                        const V3 T = sub(scale(sub(r, scale(nn, dot(nn, r))), nr), scale(nn, rt));
-                        sec.org = P;
-                        sec.dst = add(P, T);
-                        offset_point(sec.org, sec.dst);
-                        sec.state = kChildTrace; sec.lvl = rl + 1;
-                        const float c = 1 - m.Tr;
-                        sec.coef = mk(c, c, c);
-                    }
-                }
-            } else if ((f & RT_REFLECTION) && lvl < p.max_lvl) {            // :361-363
-                sec.state = kChildTrace; sec.coef = Ks; sec.lvl = lvl + 1;
-                reflection_ray(ray, P, normal, sec.org, sec.dst);
+        }
+    } else if ((f & RT_REFLECTION) && lvl < p.max_lvl) {            // :361-363
+        sec.state = kChildTrace; sec.coef = Ks; sec.lvl = lvl + 1;
+        reflection_ray(ray, P, normal, sec.org, sec.dst);
+    }
+    w.chain_local[ci] = make_float4(color.x, color.y, color.z, as_float(static_cast<int>(sec.state)));
+    if (sec.state == kChildTrace) w.chain_coef[ci] = make_float4(sec.coef.x, sec.coef.y, sec.coef.z, 0.0f);
+    else w.depth[sample] = static_cast<uint8_t>(step + 1);
+    return sec;
+}
+
+// trace() miss (:389-391): black, and the chain ends at this step.
+__device__ __forceinline__ void shade_miss(const DevWork &w, int step, int sample) {
+    w.chain_local[static_cast<int64_t>(step) * w.cap + sample] = make_float4(0, 0, 0, as_float(kChildNone));
+    w.depth[sample] = static_cast<uint8_t>(step + 1);
+}
+
+// One thread per query of the step's queue; the secondary rays go straight into the next
+// step's queue, compacted with one atomic per 1,024-query block round (a single counter word
+// takes only ~88 atomics/us, so per-wave appends are too slow).
+constexpr int kShadeBlock = 1024;
+__global__ __launch_bounds__(kShadeBlock) void k_shade(const DevScene sc, const ShadeParams p, DevWork w) {
+    const int n = w.counters[p.step];
+    const int nb = (p.step + 1) & 1;
+    for (int base = blockIdx.x * kShadeBlock; base < n; base += gridDim.x * kShadeBlock) {   // uniform per block
+        const int j = base + static_cast<int>(threadIdx.x);
+        Secondary sec;
+        sec.state = kChildNone;
+        int sample = 0;
+        const float4 qo = j < n ? w.q_org[p.step & 1][j] : make_float4(0, 0, 0, 0);
+        const float4 qd = j < n ? w.q_dst[p.step & 1][j] : make_float4(0, 0, 0, as_float(-1));
+        const int lvl = as_int(qd.w);
+        if (lvl >= 0) {                                                   // inactive (outside frame) otherwise
+            sample = as_int(qo.w);
+            int idx = w.hit_idx[j];
+            if (idx >= sc.nt) {                   // never expected: flag it for the host, do not fault
+                w.counters[kErrorSlot] = 1;
+                idx = -1;
             }
-            w.chain_local[ci] = make_float4(color.x, color.y, color.z, as_float(static_cast<int>(sec.state)));
-            if (sec.state == kChildTrace) w.chain_coef[ci] = make_float4(sec.coef.x, sec.coef.y, sec.coef.z, 0.0f);
-            else w.depth[sample] = static_cast<uint8_t>(p.step + 1);
+            if (idx < 0) {
+                shade_miss(w, p.step, sample);
+            } else {
+                sec = shade_hit(sc, p, w, p.step, sample, mk(qo.x, qo.y, qo.z), mk(qd.x, qd.y, qd.z), lvl, idx,
+                                ld3(w.hit_I[j]), [&](int l) { return w.shadow[j * p.n_lights + l] != 0; });
+            }
+        }
+        bool spawn[1] = {sec.state == kChildTrace};
+        int pos[1];
+        block_reserve_rounds<kShadeBlock, 1>(spawn, &w.counters[p.step + 1], pos);
+        if (spawn[0]) {
+            w.q_org[nb][pos[0]] = make_float4(sec.org.x, sec.org.y, sec.org.z, as_float(sample));
+            w.q_dst[nb][pos[0]] = make_float4(sec.dst.x, sec.dst.y, sec.dst.z, as_float(sec.lvl));
         }
     }
-    bool spawn[1] = {sec.state == kChildTrace};
-    int pos[1];
-    block_reserve_rounds<kShadeBlock, 1>(spawn, &w.counters[p.step + 1], pos);
-    if (spawn[0]) {
-        w.q_org[nb][pos[0]] = make_float4(sec.org.x, sec.org.y, sec.org.z, as_float(sample));
-        w.q_dst[nb][pos[0]] = make_float4(sec.dst.x, sec.dst.y, sec.dst.z, as_float(sec.lvl));
-    }
+}
+
+// Chain tail (RT_TUNE_CHAIN_FROM): the remaining steps of every query in Q_first, each lane
+// carrying its own ray through closest-hit, its shadow rays and shade until its chain ends. With
+// no launch boundary between steps, a lane's next step does not wait for the slowest wave of the
+// current one, which is what the thin last steps spend their time on. The per-ray arithmetic is
+// the per-step kernels' own (the same functions). Query counts per step (ray statistics) are
+// summed per block in LDS and added to the step counters once at the end.
+constexpr int kChainSteps = 256;   // max_lvl <= 254
+template <int W, bool kAnyHit>
+__global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_chain(
+    const DevScene sc, const ShadeParams p, DevWork w, int first, const Bvh4Node *__restrict__ n4,
+    const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx) {
+    extern __shared__ int32_t lds_stack[];
+    __shared__ int s_q[kChainSteps], s_sh[kChainSteps];
+    for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) { s_q[i] = 0; s_sh[i] = 0; }
+    __syncthreads();
+    const LaneStack stack = lane_stack(sc, lds_stack);
+    const bool shadows = (p.flags & RT_SHADOWS) && p.n_lights > 0;
+    drive_queries(w.counters[first], 0, nullptr, [&](int j, int end) {
+        if (j >= end) return;
+        const float4 qo = w.q_org[first & 1][j], qd = w.q_dst[first & 1][j];
+        int lvl = as_int(qd.w);
+        if (lvl < 0) return;
+        const int sample = as_int(qo.w);
+        V3 org = mk(qo.x, qo.y, qo.z), dst = mk(qd.x, qd.y, qd.z);
+        unsigned tests = 0, visits = 0;
+        for (int step = first; step < kChainSteps; ++step) {
+            if (step > first) atomicAdd(&s_q[step], 1);
+            int bidx = -1;
+            V3 bI = mk(0, 0, 0);
+            bvh_query_w<false, W>(sc, n4, lrec, lidx, lds_stack, org, sub(dst, org), true, bidx, bI, stack, tests, visits);
+            if (bidx >= sc.nt) { w.counters[kErrorSlot] = 1; bidx = -1; }
+            if (bidx < 0) { shade_miss(w, step, sample); break; }
+            uint32_t mask = 0;   // isShadow per light (:241-261)
+            if (shadows) {
+                atomicAdd(&s_sh[step], p.n_lights);
+                const V3 so = mk(bI.x + 0.1f, bI.y + 0.1f, bI.z + 0.1f);                // :248
+                for (int l = 0; l < p.n_lights; ++l) {
+                    int sidx = -1;
+                    V3 sI = mk(0, 0, 0);
+                    const V3 sd = mk(p.lights[l][0] - so.x, p.lights[l][1] - so.y, p.lights[l][2] - so.z);
+                    bvh_query_w<kAnyHit, W>(sc, n4, lrec, lidx, lds_stack, so, sd, true, sidx, sI, stack, tests, visits);
+                    if (sidx >= 0 && !sc.mats[sc.tri_mat[sidx]].transparent) mask |= 1u << l;   // :253-257
+                }
+            }
+            const Secondary sec = shade_hit(sc, p, w, step, sample, org, dst, lvl, bidx, bI,
+                                            [&](int l) { return ((mask >> l) & 1u) != 0; });
+            if (sec.state != kChildTrace) break;
+            org = sec.org;
+            dst = sec.dst;
+            lvl = sec.lvl;
+        }
+    });
+    __syncthreads();
+    for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) {
+        if (s_q[i]) atomicAdd(&w.counters[i], s_q[i]);
+        if (s_sh[i]) atomicAdd(&w.counters[kMaxStepsCounters + i], s_sh[i]);
     }
 }
 
@@ -1319,6 +1398,16 @@ void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int
     if (capacity <= 0) return;
     const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((capacity + kShadeBlock - 1) / kShadeBlock, 1024)));
     hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kShadeBlock), 0, stream, s, p, w);
+}
+
+void launch_chain(const DevScene &s, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
+                  hipStream_t stream) {
+    if (capacity <= 0) return;
+    const bool wide = tree_variant(s, -1) == 4;
+    auto k = wide ? (s.any_transparent ? k_chain<4, false> : k_chain<4, true>)
+                  : (s.any_transparent ? k_chain<2, false> : k_chain<2, true>);
+    hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, p, w, first,
+                       s.nodes4, s.leaf_recs, s.leaf_idx);
 }
 
 void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream) {

@@ -229,6 +229,21 @@ def test_render_accel_modes_match_golden(name, accel, workdir, gpu_available):
     _assert_image_close(u8, f32, gu8, gf32)
 
 
+@pytest.mark.parametrize("chain_from", [0, 1, 255])
+@pytest.mark.parametrize("name", ["F2b_shadow_test_160x120", "F3_spheres_128x72_pf2", "F4_refract_128x72"])
+def test_chain_tail_matches_golden(name, chain_from, workdir, gpu_available):
+    """The per-lane chain launch (RT_TUNE_CHAIN_FROM) from the first step, from the second, and
+    never: the golden frames and ray counts each time (F4 has transparent materials, so its
+    shadow rays take the closest-hit form)."""
+    entry = golden_index()[name]
+    gu8, gf32 = golden(name)
+    with R.Scene.load(scene_path(entry["scene"], workdir), device=0) as sc:
+        sc.tune("chain_from", chain_from)
+        u8, f32, counts = sc.render(_params(entry), want_f32=True)
+    assert [int(c) for c in counts] == entry["counts"]
+    _assert_image_close(u8, f32, gu8, gf32)
+
+
 def test_c4_full_frame_bvh_equals_brute_force(workdir, gpu_available):
     """The benchmark frame itself: BVH and brute-force renders of C4 1920x1080 are byte-identical
     and issue the same queries."""
@@ -279,13 +294,15 @@ def test_multi_frame_shard_batch_reassembles(workdir, gpu_available):
                                    {"pipes": 4, "xcd_split": 2}, {"shadow_virtual": 0}, {"shadow_virtual": 5},
                                    {"shadow_virtual": 0, "bvh_width": 2}, {"wave_traversal": 0},
                                    {"wave_traversal": -1}, {"wave_traversal": -1, "shadow_virtual": 0},
-                                   {"wave_traversal": -1, "lds_stack": 1}])
+                                   {"wave_traversal": -1, "lds_stack": 1}, {"chain_from": 0}, {"chain_from": 1},
+                                   {"chain_from": 3}, {"chain_from": 255}, {"chain_from": 0, "lds_stack": 1},
+                                   {"chain_from": 1, "bvh_width": 2}, {"chain_from": 0, "pipes": 1}])
 def test_launch_shape_knobs_never_change_results(knobs, workdir, gpu_available):
     """Query distribution (grid-stride, static XCD segments, work-stealing XCD queues), tiny grids
     (fewer blocks than XCDs), tree width and the LDS/HBM split of the traversal stack (1 entry in
     LDS: nearly every push overflows), render pipelines and whether shadow rays come from a
-    compacted queue or straight from the hits are placement choices only: byte-identical frames
-    and ray counts."""
+    compacted queue or straight from the hits, and from which step on the chain runs per lane in
+    one launch, are placement choices only: byte-identical frames and ray counts."""
     p = R.RenderParams(width=320, height=180, pf=2, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
     with R.Scene.load(scene_path("syn:C4", workdir), device=0) as sc:
         ref, reff, refc = sc.render(p, want_f32=True)
