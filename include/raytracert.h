@@ -208,7 +208,7 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
                                       wave (coherent rays); default 0: measured no faster on C4,
                                       primaries included (VALU-bound, not fetch-bound) */
 #define RT_TUNE_CHAIN_FROM 9     /* chain steps from this one on run in one launch, each lane carrying
-                                    its ray through closest-hit, shadows and shade (default 2;
+                                    its ray through closest-hit, shadows and shade (default 0;
                                     >= max_lvl + 1: every step its own launches) */
 #define RT_TUNE_PIPE_BATCHES 6     /* split a call into at least pipes x this many batches */
 #define RT_TUNE_PIPE_PRIORITY 7    /* 1 (default): pipelines after the first run at lower stream priority */

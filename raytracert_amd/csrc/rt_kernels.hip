@@ -1021,9 +1021,6 @@ __device__ __forceinline__ void offset_point(V3 &point, V3 dest) {   // addOffse
     point = add(point, v);
 }
 
-// One thread per query of the step's queue; the secondary rays go straight into the next
-// step's queue, compacted with one atomic per 1,024-query block round (a single counter word
-// takes only ~88 atomics/us, so per-wave appends are too slow).
 // shade (raytracing.cpp:335-368) for a hit of the chain step `step`: writes the step's chain
 // record (local colour and child state, the child's coefficient, the depth when the chain ends)
 // and returns the secondary ray, if any. is_shadowed(l) is isShadow's verdict for light l.
@@ -1174,8 +1171,11 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(const DevScene sc, const 
 // the per-step kernels' own (the same functions). Query counts per step (ray statistics) are
 // summed per block in LDS and added to the step counters once at the end.
 constexpr int kChainSteps = 256;   // max_lvl <= 254
+#ifndef RT_CHAIN_WPE
+#define RT_CHAIN_WPE 4
+#endif
 template <int W, bool kAnyHit>
-__global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_chain(
+__global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CHAIN_WPE))) void k_chain(
     const DevScene sc, const ShadeParams p, DevWork w, int first, const Bvh4Node *__restrict__ n4,
     const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx) {
     extern __shared__ int32_t lds_stack[];

@@ -229,7 +229,7 @@ def test_render_accel_modes_match_golden(name, accel, workdir, gpu_available):
     _assert_image_close(u8, f32, gu8, gf32)
 
 
-@pytest.mark.parametrize("chain_from", [0, 1, 255])
+@pytest.mark.parametrize("chain_from", [0, 1, 2, 255])
 @pytest.mark.parametrize("name", ["F2b_shadow_test_160x120", "F3_spheres_128x72_pf2", "F4_refract_128x72"])
 def test_chain_tail_matches_golden(name, chain_from, workdir, gpu_available):
     """The per-lane chain launch (RT_TUNE_CHAIN_FROM) from the first step, from the second, and
