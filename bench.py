@@ -108,7 +108,7 @@ def main():
 
     import raytracert_amd as R
     from raytracert_amd import dist as rdist, scenes
-    from raytracert_amd._capi import KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME
+    from raytracert_amd._capi import KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME, KERNEL_CHAIN
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
@@ -214,8 +214,8 @@ def main():
             render_shard()
         torch.cuda.synchronize(dev)
         scene.set_profiling(False)
-        st = {k: scene.kernel_stats(k) for k in (KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME)}
-        work = (0.0, 0.0)
+        st = {k: scene.kernel_stats(k) for k in (KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME, KERNEL_CHAIN)}
+        work = (0.0, 0.0, 0.0, 0.0)
         if scene.accel() == "bvh":   # work counters slow the kernels: count in a separate, untimed pass
             scene.reset_stats()
             scene.set_profiling(True, count_work=True)
@@ -223,11 +223,12 @@ def main():
                 render_shard()
             torch.cuda.synchronize(dev)
             scene.set_profiling(False)
-            work = scene.work_stats(KERNEL_CLOSEST_HIT)
+            work = scene.work_stats(KERNEL_CLOSEST_HIT) + scene.work_stats(KERNEL_SHADOW)
         scene.tune("pipes", args.pipes)
         return st, work
 
-    stats, (bvh_tests, bvh_visits) = profile(args.profile_steps)
+    stats, (bvh_tests, bvh_visits, sh_bvh_tests, sh_bvh_visits) = profile(args.profile_steps)
+    chain_launches, chain_ms, chain_tests = stats[KERNEL_CHAIN]
     ch_launches, ch_ms, ch_tests = stats[KERNEL_CLOSEST_HIT]
     sh_launches, sh_ms, sh_tests = stats[KERNEL_SHADOW]
     _, shade_ms, _ = stats[KERNEL_SHADE]
@@ -248,7 +249,24 @@ def main():
         total_rays = rays_per_step * args.steps
         value = total_rays / elapsed / 1e6
         queries = ch_tests / max(nt, 1)
-        if args.accel == "bvh":
+        if args.accel == "bvh" and chain_launches > 0:
+            # The chain kernel (every step of every sample per lane, RT_TUNE_CHAIN_FROM 0): per
+            # primary query 32 B in, per closest-hit query a 32-B chain record out, plus one 64-B
+            # record per node visit and per triangle test of its closest-hit and shadow queries
+            # (device counters). Roof: memory (HBM peak).
+            kname = "k_chain"
+            ch_launches, ch_ms = chain_launches, chain_ms   # the roofline's kernel from here on
+            queries = rays_by_kind[0] / world * args.profile_steps
+            tests_all, visits_all = bvh_tests + sh_bvh_tests, bvh_visits + sh_bvh_visits
+            flops = tests_all * FLOP_PER_TEST + visits_all * FLOP_PER_NODE
+            ch_bytes = (queries * 32.0 + (rays_by_kind[0] + rays_by_kind[1]) / world * args.profile_steps * 32.0 +
+                        (visits_all + tests_all) * 64.0)
+            bvh_tests, bvh_visits = tests_all, visits_all
+            ch_tests = chain_tests
+            bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
+            achieved = ch_bytes / (ch_ms / 1e3) / 1e9 if ch_ms > 0 else 0.0
+            valu = flops / (ch_ms / 1e3) / 1e12 if ch_ms > 0 else 0.0
+        elif args.accel == "bvh":
             # BVH traversal is a dependent gather: per query 32 B in + 20 B out, plus one 64-B
             # record per node visit and per triangle test (device counters). Roof: memory (HBM peak).
             kname = "k_bvh_closest_hit"
@@ -291,7 +309,7 @@ def main():
                 "scene_load_s": round(t_load, 3), "scene_gen_s": round(t_gen, 3),
             },
             "roofline": {
-                "kernel": f"{kname} (primary + secondary queries, accel={args.accel})",
+                "kernel": f"{kname} ({'every chain step: closest-hit, shadow and shade' if kname == 'k_chain' else 'primary + secondary queries'}, accel={args.accel})",
                 "bound": bound,
                 "achieved": round(achieved, 3),
                 "peak": peak,
@@ -313,10 +331,11 @@ def main():
                 "bruteforce_equivalent_TFLOPs": round(ch_tests * FLOP_PER_TEST / (ch_ms / 1e3) / 1e12, 3) if ch_ms > 0 else None,
             },
             "kernel_ms_per_step": {
-                "closest_hit": round(ch_ms / max(args.profile_steps, 1), 3),
+                "closest_hit": round(stats[KERNEL_CLOSEST_HIT][1] / max(args.profile_steps, 1), 3),
                 "shadow": round(sh_ms / max(args.profile_steps, 1), 3),
                 "shade": round(shade_ms / max(args.profile_steps, 1), 3),
                 "frame": round(frame_ms / max(args.profile_steps, 1), 3),
+                "chain": round(chain_ms / max(args.profile_steps, 1), 3),
             },
             "roofline_bruteforce": bf,
             "accel": {"mode": args.accel, "bvh": bvh_info},

@@ -223,7 +223,10 @@ int rt_scene_tune(rt_scene *scene, int32_t knob, int32_t value);
 #define RT_KERNEL_SHADOW      1   /* shadow queries (closest-hit or any-hit) */
 #define RT_KERNEL_SHADE       2   /* shading / secondary-ray generation */
 #define RT_KERNEL_FRAME       3   /* sample generation + fold + AA + quantise */
-#define RT_KERNEL_KINDS       4
+#define RT_KERNEL_CHAIN       4   /* closest-hit + shadows + shade of every step from chain_from on, per
+                                     lane in one launch (RT_TUNE_CHAIN_FROM); tests = brute-force
+                                     equivalent of all its closest-hit and shadow queries */
+#define RT_KERNEL_KINDS       5
 /* RT_PROFILE_TIMING: every launch of the scene is bracketed with hipEvents on its own stream and
  * the durations accumulated (one host sync per render call). RT_PROFILE_WORK additionally has the
  * BVH kernels count their work (rt_work_stats / rt_work_detail); the counting itself costs time,

@@ -29,7 +29,8 @@ ALL_FEATURES = 0x3F
 
 HAS_KD, HAS_KA, HAS_KS, HAS_NS, HAS_NI, HAS_TR, HAS_ILLUM = (1 << i for i in range(7))
 
-KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME = range(4)
+KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME, KERNEL_CHAIN = range(5)
+KERNEL_KINDS = 5
 ACCEL_BRUTE_FORCE, ACCEL_BVH = 0, 1
 TUNE_XCD_SPLIT, TUNE_BVH_GRID, TUNE_BVH_WIDTH, TUNE_LDS_STACK, TUNE_PIPES, TUNE_SHADOW_VIRTUAL = 0, 1, 2, 3, 4, 5
 TUNE_PIPE_BATCHES, TUNE_PIPE_PRIORITY, TUNE_WAVE_TRAVERSAL, TUNE_CHAIN_FROM = 6, 7, 8, 9

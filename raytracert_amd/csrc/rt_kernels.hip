@@ -1174,7 +1174,7 @@ constexpr int kChainSteps = 256;   // max_lvl <= 254
 #ifndef RT_CHAIN_WPE
 #define RT_CHAIN_WPE 4
 #endif
-template <int W, bool kAnyHit>
+template <int W, bool kAnyHit, bool kCount>
 __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CHAIN_WPE))) void k_chain(
     const DevScene sc, const ShadeParams p, DevWork w, int first, const Bvh4Node *__restrict__ n4,
     const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx) {
@@ -1184,6 +1184,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
     __syncthreads();
     const LaneStack stack = lane_stack(sc, lds_stack);
     const bool shadows = (p.flags & RT_SHADOWS) && p.n_lights > 0;
+    WorkTally<kCount> wc, ws;   // closest-hit and shadow work (totals only: lanes diverge here)
     drive_queries(w.counters[first], 0, nullptr, [&](int j, int end) {
         if (j >= end) return;
         const float4 qo = w.q_org[first & 1][j], qd = w.q_dst[first & 1][j];
@@ -1191,12 +1192,11 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
         if (lvl < 0) return;
         const int sample = as_int(qo.w);
         V3 org = mk(qo.x, qo.y, qo.z), dst = mk(qd.x, qd.y, qd.z);
-        unsigned tests = 0, visits = 0;
         for (int step = first; step < kChainSteps; ++step) {
             if (step > first) atomicAdd(&s_q[step], 1);
             int bidx = -1;
             V3 bI = mk(0, 0, 0);
-            bvh_query_w<false, W>(sc, n4, lrec, lidx, lds_stack, org, sub(dst, org), true, bidx, bI, stack, tests, visits);
+            bvh_query_w<false, W>(sc, n4, lrec, lidx, lds_stack, org, sub(dst, org), true, bidx, bI, stack, wc.tests, wc.visits);
             if (bidx >= sc.nt) { w.counters[kErrorSlot] = 1; bidx = -1; }
             if (bidx < 0) { shade_miss(w, step, sample); break; }
             uint32_t mask = 0;   // isShadow per light (:241-261)
@@ -1207,7 +1207,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
                     int sidx = -1;
                     V3 sI = mk(0, 0, 0);
                     const V3 sd = mk(p.lights[l][0] - so.x, p.lights[l][1] - so.y, p.lights[l][2] - so.z);
-                    bvh_query_w<kAnyHit, W>(sc, n4, lrec, lidx, lds_stack, so, sd, true, sidx, sI, stack, tests, visits);
+                    bvh_query_w<kAnyHit, W>(sc, n4, lrec, lidx, lds_stack, so, sd, true, sidx, sI, stack, ws.tests, ws.visits);
                     if (sidx >= 0 && !sc.mats[sc.tri_mat[sidx]].transparent) mask |= 1u << l;   // :253-257
                 }
             }
@@ -1219,6 +1219,8 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
             lvl = sec.lvl;
         }
     });
+    wc.flush(sc.work);
+    ws.flush(sc.work ? sc.work + kWorkFields : nullptr);
     __syncthreads();
     for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) {
         if (s_q[i]) atomicAdd(&w.counters[i], s_q[i]);
@@ -1404,8 +1406,11 @@ void launch_chain(const DevScene &s, const DevWork &w, const ShadeParams &p, int
                   hipStream_t stream) {
     if (capacity <= 0) return;
     const bool wide = tree_variant(s, -1) == 4;
-    auto k = wide ? (s.any_transparent ? k_chain<4, false> : k_chain<4, true>)
-                  : (s.any_transparent ? k_chain<2, false> : k_chain<2, true>);
+    auto k = wide ? (s.any_transparent ? k_chain<4, false, false> : k_chain<4, true, false>)
+                  : (s.any_transparent ? k_chain<2, false, false> : k_chain<2, true, false>);
+    if (s.work)
+        k = wide ? (s.any_transparent ? k_chain<4, false, true> : k_chain<4, true, true>)
+                 : (s.any_transparent ? k_chain<2, false, true> : k_chain<2, true, true>);
     hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, p, w, first,
                        s.nodes4, s.leaf_recs, s.leaf_idx);
 }

@@ -14,7 +14,7 @@ import torch  # noqa: E402,F401
 
 import raytracert_amd as R  # noqa: E402
 from raytracert_amd import scenes  # noqa: E402
-from raytracert_amd._capi import KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME  # noqa: E402
+from raytracert_amd._capi import KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME, KERNEL_CHAIN  # noqa: E402
 
 variants = json.loads(sys.argv[1]) if len(sys.argv) > 1 else [{}]
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
@@ -55,7 +55,8 @@ for r in range(rounds):
         q = {name: round(sc.kernel_stats(k)[2] / sc.counts()[1]) for name, k in
              (("ch_queries", KERNEL_CLOSEST_HIT), ("shadow_queries", KERNEL_SHADOW))}
         res[i].append({name: sc.kernel_stats(k)[1] for name, k in
-                       (("ch", KERNEL_CLOSEST_HIT), ("shadow", KERNEL_SHADOW), ("shade", KERNEL_SHADE), ("frame", KERNEL_FRAME))})
+                       (("ch", KERNEL_CLOSEST_HIT), ("shadow", KERNEL_SHADOW), ("shade", KERNEL_SHADE), ("frame", KERNEL_FRAME),
+                        ("chain", KERNEL_CHAIN))})
         res[i][-1]["wall"] = wall
         if r == 0:   # work counters slow the kernels: count once, untimed
             sc.reset_stats()
