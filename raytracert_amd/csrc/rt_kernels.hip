@@ -21,6 +21,7 @@
 #include <cstdint>
 
 #include "rt_kernels.h"
+#include "spec_pow.h"
 
 namespace rt {
 namespace {
@@ -71,11 +72,9 @@ __device__ float glibc_powf2(float x, const uint32_t *ties, int n) {
     return r;
 }
 
-// powf(SpecularTerm, Ns) (raytracing.cpp:226): evaluated in double and rounded once; agrees with
-// glibc powf except where glibc itself is not correctly rounded (colour-only, <= 1 LSB).
-__device__ __forceinline__ float spec_powf(float x, float y) {
-    return static_cast<float>(pow(static_cast<double>(x), static_cast<double>(y)));
-}
+// powf(SpecularTerm, Ns) (raytracing.cpp:226): spec_pow.h, double log2/exp2 rounded once; agrees
+// with glibc powf except where glibc itself is not correctly rounded (colour-only, <= 1 LSB).
+__device__ __forceinline__ float spec_powf(float x, float y) { return spec_pow(x, y); }
 
 // Block-wide reservation in an output queue for kPer coalesced rounds of items: round k covers
 // items base + k*BLOCK + threadIdx.x, so reads and writes stay coalesced and the output keeps
@@ -1172,7 +1171,7 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(const DevScene sc, const 
 // summed per block in LDS and added to the step counters once at the end.
 constexpr int kChainSteps = 256;   // max_lvl <= 254
 #ifndef RT_CHAIN_WPE
-#define RT_CHAIN_WPE 4
+#define RT_CHAIN_WPE 6   // measured: 6 (80 VGPRs, 36 B spill) beats 5 (92, none) and 7
 #endif
 template <int W, bool kAnyHit, bool kCount>
 __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CHAIN_WPE))) void k_chain(
