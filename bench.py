@@ -359,7 +359,7 @@ def pmc_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*_pmc.json,
     written by tools/pmc_summary.py from separate rocprofv3 --pmc passes of this bench command)."""
     import glob
-    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc.json")), key=os.path.getmtime)
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc.json")))   # round-tagged names sort by age
     for f in reversed(files):
         try:
             d = json.load(open(f))
