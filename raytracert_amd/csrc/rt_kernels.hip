@@ -1022,10 +1022,11 @@ __device__ __forceinline__ void offset_point(V3 &point, V3 dest) {   // addOffse
 
 // shade (raytracing.cpp:335-368) for a hit of the chain step `step`: writes the step's chain
 // record (local colour and child state, the child's coefficient, the depth when the chain ends)
-// and returns the secondary ray, if any. is_shadowed(l) is isShadow's verdict for light l.
+// and returns the secondary ray, if any. ray = dest - origin of the traced ray (:393);
+// is_shadowed(l) is isShadow's verdict for light l.
 template <typename Shadowed>
 __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadeParams &p, const DevWork &w, int step,
-                                               int sample, V3 origin, V3 dest, int lvl, int idx, V3 P,
+                                               int sample, V3 ray, int lvl, int idx, V3 P,
                                                Shadowed &&is_shadowed) {
     Secondary sec;
     sec.state = kChildNone;
@@ -1033,7 +1034,6 @@ __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadePa
     sec.dst = mk(0, 0, 0);
     sec.lvl = -1;
     const int64_t ci = static_cast<int64_t>(step) * w.cap + sample;
-    const V3 ray = sub(dest, origin);                                // :393
     V3 normal = ld3(sc.normals[idx]);                                // :394 (copy, mutated below)
     const DevMaterial m = sc.mats[sc.tri_mat[idx]];                  // :396
     const V3 Kd = mk(m.Kd[0], m.Kd[1], m.Kd[2]);
@@ -1149,7 +1149,7 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(const DevScene sc, const 
             if (idx < 0) {
                 shade_miss(w, p.step, sample);
             } else {
-                sec = shade_hit(sc, p, w, p.step, sample, mk(qo.x, qo.y, qo.z), mk(qd.x, qd.y, qd.z), lvl, idx,
+                sec = shade_hit(sc, p, w, p.step, sample, sub(mk(qd.x, qd.y, qd.z), mk(qo.x, qo.y, qo.z)), lvl, idx,
                                 ld3(w.hit_I[j]), [&](int l) { return w.shadow[j * p.n_lights + l] != 0; });
             }
         }
@@ -1184,8 +1184,10 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
     const LaneStack stack = lane_stack(sc, lds_stack);
     const bool shadows = (p.flags & RT_SHADOWS) && p.n_lights > 0;
     WorkTally<kCount> wc, ws;   // closest-hit and shadow work (totals only: lanes diverge here)
-    drive_queries(w.counters[first], 0, nullptr, [&](int j, int end) {
+    const int nq = w.counters[first];
+    drive_queries(nq, sc.chain_split & 3, w.wq + (2 * first) * kWqSlot, [&](int j, int end) {
         if (j >= end) return;
+        if (sc.chain_split & 4) j = nq - 1 - j;   // (diagnostic: reversed order)
         const float4 qo = w.q_org[first & 1][j], qd = w.q_dst[first & 1][j];
         int lvl = as_int(qd.w);
         if (lvl < 0) return;
@@ -1210,7 +1212,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
                     if (sidx >= 0 && !sc.mats[sc.tri_mat[sidx]].transparent) mask |= 1u << l;   // :253-257
                 }
             }
-            const Secondary sec = shade_hit(sc, p, w, step, sample, org, dst, lvl, bidx, bI,
+            const Secondary sec = shade_hit(sc, p, w, step, sample, sub(dst, org), lvl, bidx, bI,
                                             [&](int l) { return ((mask >> l) & 1u) != 0; });
             if (sec.state != kChildTrace) break;
             org = sec.org;
@@ -1218,6 +1220,285 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
             lvl = sec.lvl;
         }
     });
+    wc.flush(sc.work);
+    ws.flush(sc.work ? sc.work + kWorkFields : nullptr);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) {
+        if (s_q[i]) atomicAdd(&w.counters[i], s_q[i]);
+        if (s_sh[i]) atomicAdd(&w.counters[kMaxStepsCounters + i], s_sh[i]);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Chain with per-lane refill (RT_TUNE_CHAIN_KERNEL 1, the default). k_chain runs a lane's
+// closest-hit query, then its shadow queries, then shade, each phase to the end: a wave takes as
+// long as its slowest lane in every phase, and lanes whose chain ended idle until the whole wave's
+// 64 samples are done. Here every lane is a small state machine over one query at a time, and
+// each loop iteration is ONE traversal step of whatever query a lane holds: a four-wide node
+// visit or one triangle test. Node records and triangle records are both 64 B, so the step
+// issues one 64-B load per lane whichever it is, and the wave pays one memory latency per
+// iteration. Lanes whose query ended wait until `refill` of them are waiting (or none is
+// traversing); the wave then advances them together: record the verdict, start the next shadow
+// query, shade, start the next step's closest-hit query, or take a new sample. The per-query
+// arithmetic is bvh4_query's (node decode, cull, order) and test_triangle's, so every query's
+// result is the same; only the interleaving differs.
+// ---------------------------------------------------------------------------------------------
+struct Trav {
+    V3 o, dir, inv;
+    float pad, dlen, tcull, best;
+    int32_t ref;
+    int sp, bidx;
+    V3 bI;
+};
+
+// Start a query: the always list, then the root with bvh4_query's per-ray constants. Returns
+// false if the query is already finished (an any-hit query accepted an always-list triangle).
+__device__ __forceinline__ bool trav_begin(const DevScene &sc, Trav &t, V3 o, V3 dir, bool anyhit) {
+    t.o = o;
+    t.dir = dir;
+    t.best = FLT_MAX;
+    t.bidx = -1;
+    t.bI = mk(0, 0, 0);
+    bool done = false;
+    test_always<false>(sc, o, dir, t.best, t.bidx, t.bI, done);
+    if (anyhit && t.bidx >= 0) return false;
+    V3 inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+    constexpr float kInvMax = 0x1p100f;   // see bvh4_query
+    if (!(fabsf(inv.x) <= kInvMax)) inv.x = copysignf(kInvMax, dir.x);
+    if (!(fabsf(inv.y) <= kInvMax)) inv.y = copysignf(kInvMax, dir.y);
+    if (!(fabsf(inv.z) <= kInvMax)) inv.z = copysignf(kInvMax, dir.z);
+    t.inv = inv;
+    t.pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
+    t.dlen = sqrtf(dot(dir, dir));
+    t.tcull = INFINITY;
+    t.sp = 0;
+    t.ref = 0;
+    return true;
+}
+
+enum : unsigned { kStepNode = 1u, kStepDone = 2u };
+
+// One traversal step. Returns kStepNode if it visited a node (else it tested a triangle), plus
+// kStepDone when the query is finished. Leaf refs double as the cursor: testing the leaf's first
+// triangle leaves ref = (first + 1, count - 1).
+__device__ __forceinline__ unsigned trav_step(const Bvh4Node *__restrict__ n4, const TriRec *__restrict__ lrec,
+                                              const uint32_t *__restrict__ lidx, const LaneStack &stack, Trav &t,
+                                              bool anyhit) {
+    const bool node = t.ref >= 0;
+    const uint32_t lf = static_cast<uint32_t>(t.ref) & ((1u << kBvhCountShift) - 1u);
+    const uint4 *ptr = node ? reinterpret_cast<const uint4 *>(n4 + t.ref) : reinterpret_cast<const uint4 *>(lrec + lf);
+    const uint4 a = ptr[0], b = ptr[1], c = ptr[2], d = ptr[3];
+    if (node) {
+        const V3 o = t.o, inv = t.inv;
+        const bool nx = inv.x < 0, ny = inv.y < 0, nz = inv.z < 0;
+        const float pnx = nx ? t.pad : -t.pad, pny = ny ? t.pad : -t.pad, pnz = nz ? t.pad : -t.pad;
+        const float dx = __uint_as_float(a.x) - o.x, dy = __uint_as_float(a.y) - o.y, dz = __uint_as_float(a.z) - o.z;
+        const float kx = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w)) + 127) << 23) * inv.x;
+        const float ky = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 8)) + 127) << 23) * inv.y;
+        const float kz = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 16)) + 127) << 23) * inv.z;
+        const float cnx = (dx + pnx) * inv.x, cfx = (dx - pnx) * inv.x;
+        const float cny = (dy + pny) * inv.y, cfy = (dy - pny) * inv.y;
+        const float cnz = (dz + pnz) * inv.z, cfz = (dz - pnz) * inv.z;
+        const uint32_t wnx = nx ? b.w : b.x, wfx = nx ? b.x : b.w;   // qlo / qhi words per axis
+        const uint32_t wny = ny ? c.x : b.y, wfy = ny ? b.y : c.x;
+        const uint32_t wnz = nz ? c.y : b.z, wfz = nz ? b.z : c.y;
+        int32_t rc[4] = {static_cast<int32_t>(c.z), static_cast<int32_t>(c.w), static_cast<int32_t>(d.x),
+                         static_cast<int32_t>(d.y)};
+        float tc[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float tnx = q_decode(cnx, kx, wnx, k), tfx = q_decode(cfx, kx, wfx, k);
+            const float tny = q_decode(cny, ky, wny, k), tfy = q_decode(cfy, ky, wfy, k);
+            const float tnz = q_decode(cnz, kz, wnz, k), tfz = q_decode(cfz, kz, wfz, k);
+            const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
+            const float tx = fminf(fminf(tfx, tfy), tfz);
+            const bool h = te <= tx * 1.00001f && te <= t.tcull;   // any-hit queries keep tcull = inf
+            tc[k] = h ? fminf(te, FLT_MAX) : INFINITY;
+        }
+        const int nh = (tc[0] != INFINITY) + (tc[1] != INFINITY) + (tc[2] != INFINITY) + (tc[3] != INFINITY);
+        if (nh > 1) {
+            cswap(tc[0], rc[0], tc[1], rc[1]);
+            cswap(tc[2], rc[2], tc[3], rc[3]);
+            cswap(tc[0], rc[0], tc[2], rc[2]);
+            cswap(tc[1], rc[1], tc[3], rc[3]);
+            cswap(tc[1], rc[1], tc[2], rc[2]);
+        } else if (nh == 1) {
+            const int32_t one = tc[0] != INFINITY ? rc[0] : tc[1] != INFINITY ? rc[1] : tc[2] != INFINITY ? rc[2] : rc[3];
+            rc[0] = one;
+            tc[0] = 0.0f;
+            tc[1] = tc[2] = tc[3] = INFINITY;
+        }
+        if (tc[3] != INFINITY) stack.push(t.sp, rc[3]);
+        if (tc[2] != INFINITY) stack.push(t.sp, rc[2]);
+        if (tc[1] != INFINITY) stack.push(t.sp, rc[1]);
+        if (tc[0] != INFINITY) {
+            t.ref = rc[0];
+            return kStepNode;
+        }
+        if (t.sp == 0) return kStepNode | kStepDone;
+        t.ref = stack.pop(t.sp);
+        return kStepNode;
+    }
+    TriRec T;
+    static_assert(sizeof(TriRec) == 64, "one 64-B record per step");
+    __builtin_memcpy(&T, &a, 16);
+    __builtin_memcpy(reinterpret_cast<char *>(&T) + 16, &b, 16);
+    __builtin_memcpy(reinterpret_cast<char *>(&T) + 32, &c, 16);
+    __builtin_memcpy(reinterpret_cast<char *>(&T) + 48, &d, 16);
+    bool done = false;
+    test_triangle<false, true>(T, static_cast<int>(lidx[lf]), t.o, t.dir, t.best, t.bidx, t.bI, done);
+    if (anyhit && t.bidx >= 0) return kStepDone;
+    if (((static_cast<uint32_t>(t.ref) >> kBvhCountShift) & kBvhCountMask) > 1u) {
+        t.ref = static_cast<int32_t>(static_cast<uint32_t>(t.ref) + 1u - (1u << kBvhCountShift));
+        return 0;
+    }
+    if (t.best < FLT_MAX) t.tcull = (t.best * 1.00002f + t.pad) / t.dlen * 1.00001f;   // (any-hit: best stays FLT_MAX)
+    if (t.sp == 0) return kStepDone;
+    t.ref = stack.pop(t.sp);
+    return 0;
+}
+
+#ifndef RT_PT_WPE
+#define RT_PT_WPE 6
+#endif
+constexpr int kSupplyChunk = 64;   // samples a wave claims per atomic
+
+template <bool kAnyHit, bool kCount>
+__global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_PT_WPE))) void k_chain_pt(
+    const DevScene sc, const ShadeParams p, DevWork w, int first, int32_t *__restrict__ supply,
+    const Bvh4Node *__restrict__ n4, const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx) {
+    extern __shared__ int32_t lds_stack[];
+    __shared__ int s_q[kChainSteps], s_sh[kChainSteps];
+    for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) { s_q[i] = 0; s_sh[i] = 0; }
+    __syncthreads();
+    const LaneStack stack = lane_stack(sc, lds_stack);
+    const bool shadows = (p.flags & RT_SHADOWS) && p.n_lights > 0;
+    const int nq = w.counters[first];
+    const float4 *__restrict__ q_org = w.q_org[first & 1];
+    const float4 *__restrict__ q_dst = w.q_dst[first & 1];
+    const int lane = __lane_id();
+    const unsigned long long below = (1ull << lane) - 1ull;
+    WorkTally<kCount> wc, ws;
+    // Sample supply: the queue is cut into one segment per XCD (screen order, so an XCD's waves
+    // share a compact part of the scene in its L2); a wave claims kSupplyChunk samples at a time
+    // from its own XCD's segment, then from the others in turn (wave-uniform state).
+    const int home = blockIdx.x % kXcds;
+    const int seg_len = (nq + kXcds - 1) / kXcds;
+    int seg_k = 0, sup = 0, sup_end = 0;
+    bool dry = nq <= 0;
+    // lane state: the chain (sample, step, level; the closest hit being shaded, its shadow mask)
+    // and the query in flight (light < 0: the step's closest-hit query, else shadow query `light`)
+    bool live = false, busy = false, pend = false;
+    int sample = 0, step = first, lvl = 0, light = -1, cidx = -1;
+    uint32_t mask = 0;
+    V3 cdir = mk(0, 0, 0), cI = mk(0, 0, 0), no = mk(0, 0, 0), nd = mk(0, 0, 0);
+    Trav t;
+    t.o = t.dir = t.inv = t.bI = mk(0, 0, 0);
+    t.pad = t.dlen = t.best = 0.0f;
+    t.tcull = INFINITY;
+    t.ref = 0;
+    t.sp = 0;
+    t.bidx = -1;
+    const int refill = sc.refill;
+    while (true) {
+        if (busy) {
+            const unsigned r = trav_step(n4, lrec, lidx, stack, t, kAnyHit && light >= 0);
+            if (kCount) {
+                if (light < 0) { if (r & kStepNode) ++wc.visits; else ++wc.tests; }
+                else { if (r & kStepNode) ++ws.visits; else ++ws.tests; }
+            }
+            if (r & kStepDone) busy = false;
+        }
+        const int waiting = __popcll(__ballot(!busy && (live || !dry)));
+        if (waiting < refill && __any(busy)) continue;
+        // ---- transitions of the lanes whose query ended ----
+        if (live && !busy) {
+            if (light < 0) {   // the step's closest-hit query (trace, raytracing.cpp:381-406)
+                int bidx = t.bidx;
+                if (bidx >= sc.nt) { w.counters[kErrorSlot] = 1; bidx = -1; }   // never expected
+                if (bidx < 0) {
+                    shade_miss(w, step, sample);
+                    live = false;
+                } else {
+                    cdir = t.dir;
+                    cidx = bidx;
+                    cI = t.bI;
+                    mask = 0;
+                    light = 0;
+                    if (shadows) atomicAdd(&s_sh[step], p.n_lights);
+                }
+            } else {           // isShadow for `light` (:241-261)
+                if (t.bidx >= 0 && !sc.mats[sc.tri_mat[t.bidx]].transparent) mask |= 1u << light;   // :253-257
+                ++light;
+            }
+            if (live) {
+                if (shadows && light < p.n_lights) {   // the next light's shadow query
+                    no = mk(cI.x + 0.1f, cI.y + 0.1f, cI.z + 0.1f);                              // :248
+                    nd = mk(p.lights[light][0] - no.x, p.lights[light][1] - no.y, p.lights[light][2] - no.z);
+                    pend = true;
+                } else {                                // every verdict known: shade
+                    const Secondary sec = shade_hit(sc, p, w, step, sample, cdir, lvl, cidx, cI,
+                                                    [&](int l) { return ((mask >> l) & 1u) != 0; });
+                    if (sec.state == kChildTrace && step + 1 < kChainSteps) {
+                        ++step;
+                        lvl = sec.lvl;
+                        light = -1;
+                        atomicAdd(&s_q[step], 1);
+                        no = sec.org;
+                        nd = sub(sec.dst, sec.org);
+                        pend = true;
+                    } else {
+                        live = false;
+                    }
+                }
+            }
+        }
+        // ---- lanes without a chain take the next samples, in lane order ----
+        while (!dry) {
+            const unsigned long long need = __ballot(!live);
+            if (!need) break;
+            if (sup >= sup_end) {
+                bool got = false;
+                while (seg_k < kXcds) {
+                    const int g = (home + seg_k) % kXcds;
+                    const int begin = min(nq, g * seg_len), end = min(nq, begin + seg_len);
+                    int b = 0;
+                    if (lane == 0) b = atomicAdd(&supply[g * kWqStride], kSupplyChunk);
+                    b = begin + __shfl(b, 0);
+                    if (b < end) {
+                        sup = b;
+                        sup_end = min(end, b + kSupplyChunk);
+                        got = true;
+                        break;
+                    }
+                    ++seg_k;
+                }
+                if (!got) { dry = true; break; }
+            }
+            const int take = min(__popcll(need), sup_end - sup);
+            const int rank = __popcll(need & below);
+            if (!live && rank < take) {
+                const int j = sup + rank;
+                const float4 qo = q_org[j], qd = q_dst[j];
+                if (as_int(qd.w) >= 0) {   // else outside the frame: no chain
+                    sample = as_int(qo.w);
+                    lvl = as_int(qd.w);
+                    step = first;
+                    light = -1;
+                    live = true;
+                    no = mk(qo.x, qo.y, qo.z);
+                    nd = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);
+                    pend = true;
+                }
+            }
+            sup += take;
+        }
+        if (pend) {
+            pend = false;
+            busy = trav_begin(sc, t, no, nd, kAnyHit && light >= 0);
+        }
+        if (dry && !__any(live)) break;
+    }
     wc.flush(sc.work);
     ws.flush(sc.work ? sc.work + kWorkFields : nullptr);
     __syncthreads();
@@ -1405,6 +1686,13 @@ void launch_chain(const DevScene &s, const DevWork &w, const ShadeParams &p, int
                   hipStream_t stream) {
     if (capacity <= 0) return;
     const bool wide = tree_variant(s, -1) == 4;
+    if (wide && s.chain_kernel == 1) {
+        auto k = s.any_transparent ? k_chain_pt<false, false> : k_chain_pt<true, false>;
+        if (s.work) k = s.any_transparent ? k_chain_pt<false, true> : k_chain_pt<true, true>;
+        hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, p, w, first,
+                           w.wq + (2 * first) * kWqSlot, s.nodes4, s.leaf_recs, s.leaf_idx);
+        return;
+    }
     auto k = wide ? (s.any_transparent ? k_chain<4, false, false> : k_chain<4, true, false>)
                   : (s.any_transparent ? k_chain<2, false, false> : k_chain<2, true, false>);
     if (s.work)

@@ -22,6 +22,8 @@ spec = getattr(scenes, sys.argv[3]) if len(sys.argv) > 3 else scenes.C4
 obj = scenes.write_sphere_grid(spec, tempfile.mkdtemp(), "ab")
 sc = R.Scene.load(obj, device=0)
 p = R.RenderParams(width=1920, height=1080, pf=1, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
+for k, val in json.loads(os.environ.get("AB_REF", "{}")).items():   # knobs of the reference image
+    sc.tune(k, val)
 ref, _, _ = sc.render(p)
 layout_tiles = ((p.width + 15) // 16) * ((p.height + 15) // 16)
 dbuf = torch.zeros(layout_tiles * 16 * 16 * 3, dtype=torch.uint8, device="cuda:0")
