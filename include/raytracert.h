@@ -214,6 +214,8 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
                                     phase (closest, shadows, shade); 1: every lane stays busy, one
                                     traversal step per iteration, and lanes whose query ended are
                                     refilled (measured slower: lanes drift apart, L1 misses x3.7) */
+#define RT_TUNE_TOP_NODES 13     /* four-wide nodes of the tree's top levels (breadth-first, the first
+                                    ones in the node array) each block reads from an LDS copy (0-85) */
 #define RT_TUNE_CHAIN_SPLIT 12   /* query distribution of the phased chain launch, as RT_TUNE_XCD_SPLIT */
 #define RT_TUNE_REFILL 11        /* chain kernel 1: lanes of a wave waiting before it advances them (1-64) */
 #define RT_TUNE_PIPE_BATCHES 6     /* split a call into at least pipes x this many batches */
@@ -253,6 +255,10 @@ int rt_work_stats(rt_scene *scene, int32_t kind, double *tests, double *node_vis
  * tasks, [5] sum over wave tasks of the largest per-query test count. */
 #define RT_WORK_FIELDS 6
 int rt_work_detail(rt_scene *scene, int32_t kind, uint64_t out[RT_WORK_FIELDS]);
+/* Diagnostic words written by diagnostic kernel builds (e.g. -DRT_WAVE_TIMES: per-wave start and
+ * end clocks of the chain launch) while profiling is RT_PROFILE_WORK; 0 in production builds.
+ * Reads count words from offset (offset + count <= 131072); synchronises the device. */
+int rt_diag_read(rt_scene *scene, int64_t offset, int64_t count, uint64_t *out);
 
 #ifdef __cplusplus
 }

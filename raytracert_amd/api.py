@@ -245,7 +245,7 @@ class Scene:
              "pipe_batches": _capi.TUNE_PIPE_BATCHES, "pipe_priority": _capi.TUNE_PIPE_PRIORITY,
              "wave_traversal": _capi.TUNE_WAVE_TRAVERSAL, "chain_from": _capi.TUNE_CHAIN_FROM,
              "chain_kernel": _capi.TUNE_CHAIN_KERNEL, "refill": _capi.TUNE_REFILL,
-             "chain_split": _capi.TUNE_CHAIN_SPLIT}[knob]
+             "chain_split": _capi.TUNE_CHAIN_SPLIT, "top_nodes": _capi.TUNE_TOP_NODES}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
 
     def bvh_digest(self) -> int:
@@ -278,6 +278,12 @@ class Scene:
         t, v = C.c_double(), C.c_double()
         check(lib().rt_work_stats(self._h, kind, C.byref(t), C.byref(v)))
         return t.value, v.value
+
+    def diag_read(self, offset: int, count: int) -> np.ndarray:
+        """Diagnostic words of a diagnostic kernel build (rt_diag_read)."""
+        d = np.zeros(count, np.uint64)
+        check(lib().rt_diag_read(self._h, offset, count, _ptr(d)))
+        return d
 
     def work_detail(self, kind: int = _capi.KERNEL_CLOSEST_HIT) -> dict:
         """Full BVH work counters of `kind` (rt_work_detail): tests, visits, the per-wave-task

@@ -343,6 +343,39 @@ struct Collapser {
     }
 };
 
+// Renumber the four-wide nodes so the top `levels` levels come first in breadth-first order
+// (the root stays 0); deeper nodes keep their depth-first order. Kernels keep a prefix of the
+// node array in LDS (DevScene::top_nodes), so the prefix must be the levels every query visits.
+void top_levels_first(std::vector<Bvh4Node> &nodes, int levels) {
+    const size_t n = nodes.size();
+    if (n <= 1) return;
+    std::vector<int> order{0}, lvl{0};
+    std::vector<char> top(n, 0);
+    top[0] = 1;
+    for (size_t head = 0; head < order.size(); ++head) {
+        if (lvl[head] + 1 >= levels) continue;
+        const Bvh4Node &g = nodes[order[head]];
+        for (int c = 0; c < 4; ++c) {
+            const int32_t r = g.child[c];
+            if (r < 0 || top[r]) continue;   // leaf, empty slot
+            top[r] = 1;
+            order.push_back(r);
+            lvl.push_back(lvl[head] + 1);
+        }
+    }
+    for (size_t i = 0; i < n; ++i)
+        if (!top[i]) order.push_back(static_cast<int>(i));
+    std::vector<int32_t> id(n);
+    for (size_t k = 0; k < n; ++k) id[order[k]] = static_cast<int32_t>(k);
+    std::vector<Bvh4Node> out(n);
+    for (size_t k = 0; k < n; ++k) {
+        out[k] = nodes[order[k]];
+        for (int c = 0; c < 4; ++c)
+            if (out[k].child[c] >= 0) out[k].child[c] = id[out[k].child[c]];
+    }
+    nodes.swap(out);
+}
+
 }  // namespace
 
 float bvh4_decode(float origin, int ex, uint32_t q) {
@@ -456,6 +489,7 @@ int build_bvh(const HostScene &s, const std::vector<TriRec> &recs, HostBvh &out)
         c.run(0, 1);
         if (!c.ok) return RT_E_ARG;   // a box no 8-bit grid can bound (coordinates near FLT_MAX)
         out.depth4 = c.depth;
+        top_levels_first(out.nodes4, kTopLevels4);
     }
     if (b.nodes[0].left < 0) {   // the whole tree is one leaf: wrap it in a root with an empty sibling
         BvhNode root{};

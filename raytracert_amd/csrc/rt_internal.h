@@ -63,6 +63,8 @@ constexpr uint32_t kBvhLeafBit = 0x80000000u;    // child ref: leaf | count << 2
 constexpr int kBvhCountShift = 21;
 constexpr uint32_t kBvhCountMask = 0x3FFu;
 constexpr int32_t kBvhEmpty = static_cast<int32_t>(kBvhLeafBit);   // a leaf with no triangles
+constexpr int kTopLevels4 = 4;                   // four-wide levels stored first, breadth-first (<= 85 nodes)
+constexpr int kMaxTopNodes = 85;                 // RT_TUNE_TOP_NODES bound (LDS copy of the node array's prefix)
 
 // Two children per node, both boxes stored in the parent (64 B).
 struct alignas(16) BvhNode {

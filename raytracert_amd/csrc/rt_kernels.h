@@ -83,6 +83,7 @@ struct DevScene {
     int32_t chain_kernel;           // RT_TUNE_CHAIN_KERNEL: 0 phased per-lane chain, 1 per-lane refill
     int32_t refill;                 // RT_TUNE_REFILL: waiting lanes before a refill wave advances them
     int32_t chain_split;            // RT_TUNE_CHAIN_SPLIT: query distribution of k_chain (as xcd_split)
+    int32_t top_nodes;              // RT_TUNE_TOP_NODES: four-wide nodes [0, top_nodes) read from an LDS copy
 };
 
 struct DevWork {
@@ -103,6 +104,7 @@ struct DevWork {
 constexpr int kMaxStepsCounters = 4096;   // counters[step] for main queues; [kMaxStepsCounters + step] shadow
 constexpr int kErrorSlot = 2 * kMaxStepsCounters - 1;   // set by kernels on an internal inconsistency
 constexpr int kWorkFields = 6;               // = RT_WORK_FIELDS
+constexpr int kDiagWords = 1 << 17;          // diagnostic words after the work counters (rt_diag_read)
 constexpr int kWqStride = 16;                // one 64-B line per segment counter
 constexpr int kWqSlot = 8 * kWqStride;       // eight segments (one per XCD) per launch
 

@@ -202,6 +202,8 @@ struct LaneStack {
     int32_t (*lds)[kBvhBlock];
     int32_t *ovf;
     int cap, stride, gl;
+    const uint4 *top;   // LDS copy of the four-wide node array's first ntop nodes (the top levels)
+    int ntop;
     __device__ __forceinline__ void push(int &sp, int32_t v) const {
         if (sp < cap) lds[sp][threadIdx.x] = v;
         else ovf[static_cast<size_t>(sp - cap) * stride + gl] = v;
@@ -217,6 +219,8 @@ struct LaneStack {
     }
 };
 
+// Dynamic LDS of the per-lane BVH kernels: [lds_stack entries][128 lanes] of stack, then the top
+// nodes. Every thread of the block must call this before its first query (barrier).
 __device__ __forceinline__ LaneStack lane_stack(const DevScene &sc, int32_t *lds) {
     LaneStack st;
     st.lds = reinterpret_cast<int32_t (*)[kBvhBlock]>(lds);
@@ -224,7 +228,27 @@ __device__ __forceinline__ LaneStack lane_stack(const DevScene &sc, int32_t *lds
     st.cap = sc.lds_stack;
     st.stride = static_cast<int>(gridDim.x) * kBvhBlock;
     st.gl = static_cast<int>(blockIdx.x) * kBvhBlock + static_cast<int>(threadIdx.x);
+    uint4 *top = reinterpret_cast<uint4 *>(lds + static_cast<size_t>(max(sc.lds_stack, 1)) * kBvhBlock);
+    st.top = top;
+    st.ntop = sc.top_nodes;
+    if (sc.top_nodes > 0) {
+        const uint4 *__restrict__ src = reinterpret_cast<const uint4 *>(sc.nodes4);
+        for (int i = threadIdx.x; i < 4 * sc.top_nodes; i += blockDim.x) top[i] = src[i];
+        __syncthreads();
+    }
     return st;
+}
+
+// A four-wide node's 64 bytes: from the LDS copy for the top levels, else from the node array.
+__device__ __forceinline__ void load_node4(const LaneStack &stack, const Bvh4Node *__restrict__ nodes4, int32_t ref,
+                                           uint4 &a, uint4 &b, uint4 &c, uint4 &d) {
+    if (ref < stack.ntop) {
+        const uint4 *p = stack.top + 4 * ref;
+        a = p[0]; b = p[1]; c = p[2]; d = p[3];
+    } else {
+        const uint4 *p = reinterpret_cast<const uint4 *>(nodes4 + ref);
+        a = p[0]; b = p[1]; c = p[2]; d = p[3];
+    }
 }
 
 __device__ __forceinline__ bool box_hit(const RayBox &R, float lx, float ly, float lz, float hx, float hy, float hz,
@@ -268,9 +292,25 @@ __device__ __forceinline__ void test_always(const DevScene &sc, V3 o, V3 dir, fl
 // reaches the comparison with the current best.
 // (Skipping the divisions when their outcome is decided by signs or approximate quotients was
 // measured slower: the extra branches and registers cost more than the divisions they save.)
+#ifndef RT_LEAF_PAIRS
+#define RT_LEAF_PAIRS 0   // measured neutral on C4 (0.88 vs 0.89 ms), costs VGPRs
+#endif
 template <bool kAnyHit>
 __device__ __forceinline__ void test_leaf(const DevScene &sc, int first, int cnt, V3 o, V3 dir, float &best, int &bidx,
                                           V3 &bI, bool &done) {
+    if (RT_LEAF_PAIRS) {
+        // Two records per round, both loads in flight before either test (the second load repeats
+        // the last record when the count is odd; its test is skipped). The lexicographic minimum
+        // does not depend on the order of the tests.
+        for (int k = 0; k < cnt; k += 2) {
+            const int k1 = min(k + 1, cnt - 1);
+            const TriRec A = sc.leaf_recs[first + k];
+            const TriRec B = sc.leaf_recs[first + k1];
+            test_triangle<kAnyHit, true>(A, static_cast<int>(sc.leaf_idx[first + k]), o, dir, best, bidx, bI, done);
+            if (k1 != k) test_triangle<kAnyHit, true>(B, static_cast<int>(sc.leaf_idx[first + k1]), o, dir, best, bidx, bI, done);
+        }
+        return;
+    }
     for (int k = 0; k < cnt; ++k) {
         const TriRec T = sc.leaf_recs[first + k];
         test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first + k]), o, dir, best, bidx, bI, done);
@@ -346,9 +386,29 @@ __device__ __forceinline__ void cswap(float &ta, int32_t &ra, float &tb, int32_t
     ra = r;
 }
 
+// Diagnostic build only (-DRT_STAMPS): per-lane shader-clock sums of bvh4_query's phases, read
+// through the counting instantiation of k_bvh_intersect_only (rt_work_detail, shadow fields):
+// [0] node data wait, [1] node arithmetic + stack, [2] triangle data wait, [4] triangle arithmetic,
+// [5] whole queries. The stamps serialise the loop (s_waitcnt before each), so they split a step's
+// time into its parts; they do not measure the production schedule.
+struct Stamps { unsigned long long v[6]; };
+#ifdef RT_STAMPS
+constexpr bool kStamps = true;
+#else
+constexpr bool kStamps = false;
+#endif
+#ifdef RT_STAMPS
+#define RT_STAMP(t) do { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); (t) = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define RT_STAMP(t) do { (t) = 0; } while (0)
+#endif
+
 template <bool kAnyHit>
 __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, bool active, int &bidx, V3 &bI,
-                                           const LaneStack &stack, unsigned &tests, unsigned &visits) {
+                                           const LaneStack &stack, unsigned &tests, unsigned &visits,
+                                           Stamps *st = nullptr) {
+    unsigned long long q0 = 0, s0 = 0, s1 = 0, s2 = 0;
+    if (st) RT_STAMP(q0);
     float best = FLT_MAX;
     bool done = !active;
     test_always<kAnyHit>(sc, o, dir, best, bidx, bI, done);
@@ -375,8 +435,14 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
     while (true) {
         if (ref >= 0) {
             ++visits;
-            const uint4 *np = reinterpret_cast<const uint4 *>(sc.nodes4 + ref);
-            const uint4 a = np[0], b = np[1], c = np[2], d = np[3];
+            if (st) RT_STAMP(s0);
+            uint4 a, b, c, d;
+            load_node4(stack, sc.nodes4, ref, a, b, c, d);
+            if (st) {
+                asm volatile("" ::"v"(a.x), "v"(b.x), "v"(c.x), "v"(d.x));
+                RT_STAMP(s1);
+                st->v[0] += s1 - s0;
+            }
             const float dx = __uint_as_float(a.x) - o.x, dy = __uint_as_float(a.y) - o.y, dz = __uint_as_float(a.z) - o.z;
             const float kx = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w)) + 127) << 23) * inv.x;
             const float ky = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 8)) + 127) << 23) * inv.y;
@@ -422,9 +488,13 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
                 if (tc[0] != INFINITY) {
                     ref = rc[0];
                 } else {
-                    if (sp == 0) break;
+                    if (sp == 0) {
+                        if (st) { RT_STAMP(s2); st->v[1] += s2 - s1; }
+                        break;
+                    }
                     ref = stack.pop(sp);
                 }
+                if (st) { RT_STAMP(s2); st->v[1] += s2 - s1; }
             } else {   // any-hit: any order finds the same verdict; visit the first wanted child
                 int32_t nxt = kBvhEmpty;
                 bool have = false;
@@ -447,7 +517,22 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
             const uint32_t u = static_cast<uint32_t>(ref);
             const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
             const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
-            test_leaf<kAnyHit>(sc, first, cnt, o, dir, best, bidx, bI, done);
+            if (st) {
+#ifdef RT_STAMPS
+                for (int k = 0; k < cnt; ++k) {
+                    RT_STAMP(s0);
+                    const TriRec T = sc.leaf_recs[first + k];
+                    asm volatile("" ::"v"(T.t0[0]), "v"(T.u[0]), "v"(T.v[0]), "v"(T.n[0]));
+                    RT_STAMP(s1);
+                    test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first + k]), o, dir, best, bidx, bI, done);
+                    RT_STAMP(s2);
+                    st->v[2] += s1 - s0;
+                    st->v[4] += s2 - s1;
+                }
+#endif
+            } else {
+                test_leaf<kAnyHit>(sc, first, cnt, o, dir, best, bidx, bI, done);
+            }
             if (!kAnyHit && best < FLT_MAX) tcull = (best * 1.00002f + pad) / dlen * 1.00001f;
             tests += static_cast<unsigned>(cnt);
             if (kAnyHit && done) break;
@@ -455,6 +540,7 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
             ref = stack.pop(sp);
         }
     }
+    if (st) { RT_STAMP(s0); st->v[5] += s0 - q0; }
 }
 
 
@@ -572,10 +658,11 @@ template <bool kAnyHit, int W>
 __device__ __forceinline__ void bvh_query_w(const DevScene &sc, const Bvh4Node *__restrict__ n4,
                                             const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx,
                                             int32_t *lds, V3 o, V3 dir, bool active, int &bidx, V3 &bI,
-                                            const LaneStack &stack, unsigned &tests, unsigned &visits) {
+                                            const LaneStack &stack, unsigned &tests, unsigned &visits,
+                                            Stamps *st = nullptr) {
     if (W == 5) wave_query<kAnyHit>(sc, n4, lrec, lidx, o, dir, active, bidx, bI, lds + (threadIdx.x >> 6) * sc.bvh4_stack,
                                     tests, visits);
-    else if (W == 4) bvh4_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
+    else if (W == 4) bvh4_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits, st);
     else bvh_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
 }
 
@@ -653,7 +740,7 @@ struct QueryCursor {
     int n, split, k = 0, base, step, end;
     int32_t *wq;
     __device__ __forceinline__ QueryCursor(int n_, int split_, int32_t *wq_) : n(n_), split(split_), wq(wq_) {
-        if (split == 2 && wq) return;
+        if ((split == 2 || split == 3) && wq) return;
         const Segment seg = xcd_segment(n, kBvhBlock, split == 1);
         base = seg.start - seg.step;
         step = seg.step;
@@ -661,6 +748,15 @@ struct QueryCursor {
     }
     // Next query index for this lane (may be >= end: inactive lane); false once the wave is done.
     __device__ __forceinline__ bool next(int &j) {
+        if (split == 3 && wq) {   // 64-query chunks dealt round-robin to the XCDs, taken dynamically within each
+            const int g = blockIdx.x % kXcds;
+            int c = 0;
+            if (__lane_id() == 0) c = atomicAdd(&wq[g * kWqStride], 1);
+            const int b = (__shfl(c, 0) * kXcds + g) * kWave;
+            end = n;
+            if (b < n) { j = b + __lane_id(); return true; }
+            return false;
+        }
         if (split == 2 && wq) {
             const int home = blockIdx.x % kXcds;
             const int chunk = (n + kXcds - 1) / kXcds;
@@ -798,6 +894,7 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_intersect_only(const DevScene
     extern __shared__ int32_t lds_stack[];
     const LaneStack stack = lane_stack(sc, lds_stack);
     WorkTally<kCount> wt;
+    Stamps stamps = {};
     drive_queries(n, 0, nullptr, [&](int j, int end) {
         const bool active = j < end;
         V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
@@ -809,11 +906,19 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_intersect_only(const DevScene
         int bidx = -1;
         V3 bI = mk(0, 0, 0);
         wt.begin();
-        bvh_query_w<false, W>(sc, n4, lrec, lidx, lds_stack, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
+        bvh_query_w<false, W>(sc, n4, lrec, lidx, lds_stack, o, dir, active, bidx, bI, stack, wt.tests, wt.visits,
+                              kStamps && kCount ? &stamps : nullptr);
         wt.end();
         if (active) { idx[j] = bidx; I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f); }
     });
     wt.flush(sc.work);
+    if (kStamps && kCount && sc.work) {   // (diagnostic build) per-wave sums into the shadow fields
+        for (int f = 0; f < 6; ++f) {
+            unsigned long long v = stamps.v[f];
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if (__lane_id() == 0 && f != 3) atomicAdd(&sc.work[kWorkFields + f], v);
+        }
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_closest_hit(const TriRec *__restrict__ tris, int nt,
@@ -1184,6 +1289,12 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
     const LaneStack stack = lane_stack(sc, lds_stack);
     const bool shadows = (p.flags & RT_SHADOWS) && p.n_lights > 0;
     WorkTally<kCount> wc, ws;   // closest-hit and shadow work (totals only: lanes diverge here)
+#ifdef RT_WAVE_TIMES   // diagnostic build: each wave's start / end clock (100 MHz) and query count
+    unsigned long long *wt_out = sc.work ? sc.work + 2 * kWorkFields + 3 * ((blockIdx.x * kBvhBlock + threadIdx.x) >> 6) : nullptr;
+    if (wt_out && (3 * ((blockIdx.x * kBvhBlock + threadIdx.x) >> 6) + 3 > kDiagWords)) wt_out = nullptr;
+    if (wt_out && __lane_id() == 0) wt_out[0] = __builtin_amdgcn_s_memrealtime();
+    unsigned long long wt_q = 0;
+#endif
     const int nq = w.counters[first];
     drive_queries(nq, sc.chain_split & 3, w.wq + (2 * first) * kWqSlot, [&](int j, int end) {
         if (j >= end) return;
@@ -1191,6 +1302,9 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
         const float4 qo = w.q_org[first & 1][j], qd = w.q_dst[first & 1][j];
         int lvl = as_int(qd.w);
         if (lvl < 0) return;
+#ifdef RT_WAVE_TIMES
+        ++wt_q;
+#endif
         const int sample = as_int(qo.w);
         V3 org = mk(qo.x, qo.y, qo.z), dst = mk(qd.x, qd.y, qd.z);
         for (int step = first; step < kChainSteps; ++step) {
@@ -1220,6 +1334,16 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
             lvl = sec.lvl;
         }
     });
+#ifdef RT_WAVE_TIMES
+    for (int off = 32; off > 0; off >>= 1) wt_q += __shfl_xor(wt_q, off);
+    // HW_ID (hwreg 4): wave slot [3:0], SIMD [5:4], CU [11:8], SE [15:13] (gfx9 layout); XCC_ID (hwreg 20)
+    const unsigned hwid = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+    const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));
+    if (wt_out && __lane_id() == 0) {
+        wt_out[1] = __builtin_amdgcn_s_memrealtime();
+        wt_out[2] = wt_q | (static_cast<unsigned long long>(hwid) << 32) | (static_cast<unsigned long long>(xcc & 0xF) << 60);
+    }
+#endif
     wc.flush(sc.work);
     ws.flush(sc.work ? sc.work + kWorkFields : nullptr);
     __syncthreads();
@@ -1286,8 +1410,14 @@ __device__ __forceinline__ unsigned trav_step(const Bvh4Node *__restrict__ n4, c
                                               bool anyhit) {
     const bool node = t.ref >= 0;
     const uint32_t lf = static_cast<uint32_t>(t.ref) & ((1u << kBvhCountShift) - 1u);
-    const uint4 *ptr = node ? reinterpret_cast<const uint4 *>(n4 + t.ref) : reinterpret_cast<const uint4 *>(lrec + lf);
-    const uint4 a = ptr[0], b = ptr[1], c = ptr[2], d = ptr[3];
+    uint4 a, b, c, d;
+    if (node && t.ref < stack.ntop) {
+        const uint4 *p = stack.top + 4 * t.ref;
+        a = p[0]; b = p[1]; c = p[2]; d = p[3];
+    } else {
+        const uint4 *ptr = node ? reinterpret_cast<const uint4 *>(n4 + t.ref) : reinterpret_cast<const uint4 *>(lrec + lf);
+        a = ptr[0]; b = ptr[1]; c = ptr[2]; d = ptr[3];
+    }
     if (node) {
         const V3 o = t.o, inv = t.inv;
         const bool nx = inv.x < 0, ny = inv.y < 0, nz = inv.z < 0;
@@ -1586,7 +1716,14 @@ void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevW
 }
 
 // LDS part of the traversal stack: lds_stack entries per lane (the rest overflows to global)
-inline size_t bvh_lds(const DevScene &s) { return sizeof(int32_t) * kBvhBlock * static_cast<size_t>(std::max(s.lds_stack, 1)); }
+inline size_t bvh_lds(const DevScene &s) {
+    return sizeof(int32_t) * kBvhBlock * static_cast<size_t>(std::max(s.lds_stack, 1)) + sizeof(Bvh4Node) * static_cast<size_t>(s.top_nodes);
+}
+// The LDS node cache holds four-wide nodes: off for the other tree kernels.
+inline DevScene for_width(DevScene s, int W) {
+    if (W != 4) s.top_nodes = 0;
+    return s;
+}
 
 // 128-thread blocks with a 10-20 KB LDS stack: 16 resident per CU (32 waves) -> 4096 blocks.
 constexpr int kMaxBvhGrid = 4096;
@@ -1611,7 +1748,8 @@ inline size_t tree_lds(const DevScene &s, int W) {
 }
 
 template <int W>
-void launch_ch(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
+void launch_ch(const DevScene &s0, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
+    const DevScene s = for_width(s0, W);
     auto k = s.work ? k_bvh_closest_hit<W, true> : k_bvh_closest_hit<W, false>;
     hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), tree_lds(s, W), stream, s,
                        w.q_org[step & 1], w.q_dst[step & 1], &w.counters[step], w.hit_idx, w.hit_I,
@@ -1638,8 +1776,9 @@ void launch_shadow_gen(const DevScene &, const DevWork &w, const ShadeParams &p,
 }
 
 template <int W>
-void launch_sh(const DevScene &s, const DevWork &w, const ShadowSource &src, int step, int64_t capacity,
+void launch_sh(const DevScene &s0, const DevWork &w, const ShadowSource &src, int step, int64_t capacity,
                hipStream_t stream) {
+    const DevScene s = for_width(s0, W);
     auto k = s.any_transparent ? k_bvh_shadow_hit<false, W, false> : k_bvh_shadow_hit<true, W, false>;
     if (s.work) k = s.any_transparent ? k_bvh_shadow_hit<false, W, true> : k_bvh_shadow_hit<true, W, true>;
     hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), tree_lds(s, W), stream, s, src, w.shadow,
@@ -1682,10 +1821,11 @@ void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int
     hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kShadeBlock), 0, stream, s, p, w);
 }
 
-void launch_chain(const DevScene &s, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
+void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
                   hipStream_t stream) {
     if (capacity <= 0) return;
-    const bool wide = tree_variant(s, -1) == 4;
+    const bool wide = tree_variant(s0, -1) == 4;
+    const DevScene s = for_width(s0, wide ? 4 : 2);
     if (wide && s.chain_kernel == 1) {
         auto k = s.any_transparent ? k_chain_pt<false, false> : k_chain_pt<true, false>;
         if (s.work) k = s.any_transparent ? k_chain_pt<false, true> : k_chain_pt<true, true>;
@@ -1713,11 +1853,12 @@ void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t strea
     hipLaunchKernelGGL(k_fold_rays, dim3(grid_for(n)), dim3(kBlock), 0, stream, w, n, rgb);
 }
 
-void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *dst, int32_t n, int32_t *idx,
+void launch_intersect_only(const DevScene &s0, const float4 *org, const float4 *dst, int32_t n, int32_t *idx,
                            float4 *I, hipStream_t stream) {
     if (n <= 0) return;
-    if (s.use_bvh) {
-        const int W = tree_variant(s, 31);
+    if (s0.use_bvh) {
+        const int W = tree_variant(s0, 31);
+        const DevScene s = for_width(s0, W);
         auto k = W == 5 ? (s.work ? k_bvh_intersect_only<5, true> : k_bvh_intersect_only<5, false>)
                  : W == 4 ? (s.work ? k_bvh_intersect_only<4, true> : k_bvh_intersect_only<4, false>)
                           : (s.work ? k_bvh_intersect_only<2, true> : k_bvh_intersect_only<2, false>);
@@ -1725,7 +1866,7 @@ void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *d
                            s.nodes4, s.leaf_recs, s.leaf_idx);
         return;
     }
-    hipLaunchKernelGGL(k_intersect_only, dim3(grid_for(n)), dim3(kBlock), 0, stream, s.tris, s.nt, org, dst, n, idx, I);
+    hipLaunchKernelGGL(k_intersect_only, dim3(grid_for(n)), dim3(kBlock), 0, stream, s0.tris, s0.nt, org, dst, n, idx, I);
 }
 
 }  // namespace rt
