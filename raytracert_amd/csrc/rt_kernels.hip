@@ -376,6 +376,18 @@ __device__ __forceinline__ float q_decode(float base, float scale, uint32_t word
     return fmaf(static_cast<float>((word >> (8 * c)) & 0xFFu), scale, base);   // q * scale is exact
 }
 
+#ifndef RT_PACKED_SLABS
+#define RT_PACKED_SLABS 0   // measured 4% slower on C4 (v_pk_fma_f32 costs two issue slots)
+#endif
+#if RT_PACKED_SLABS
+typedef float f2 __attribute__((ext_vector_type(2)));
+// q_decode for children c and c + 1 at once
+__device__ __forceinline__ f2 q_decode2(float base, float scale, uint32_t word, int c) {
+    const f2 q = f2{static_cast<float>((word >> (8 * c)) & 0xFFu), static_cast<float>((word >> (8 * c + 8)) & 0xFFu)};
+    return __builtin_elementwise_fma(q, f2{scale, scale}, f2{base, base});
+}
+#endif
+
 __device__ __forceinline__ void cswap(float &ta, int32_t &ra, float &tb, int32_t &rb) {
     const bool sw = tb < ta;
     const float t = sw ? tb : ta;
@@ -456,6 +468,22 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
             int32_t rc[4] = {static_cast<int32_t>(c.z), static_cast<int32_t>(c.w), static_cast<int32_t>(d.x),
                              static_cast<int32_t>(d.y)};
             float tc[4];
+#if RT_PACKED_SLABS
+            // children in pairs through packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: IEEE per element,
+            // so every bound is the same value as q_decode's)
+#pragma unroll
+            for (int k = 0; k < 4; k += 2) {
+                const f2 tnx = q_decode2(cnx, kx, wnx, k), tfx = q_decode2(cfx, kx, wfx, k);
+                const f2 tny = q_decode2(cny, ky, wny, k), tfy = q_decode2(cfy, ky, wfy, k);
+                const f2 tnz = q_decode2(cnz, kz, wnz, k), tfz = q_decode2(cfz, kz, wfz, k);
+                const f2 te = f2{fmaxf(fmaxf(fmaxf(tnx.x, tny.x), tnz.x), 0.0f), fmaxf(fmaxf(fmaxf(tnx.y, tny.y), tnz.y), 0.0f)};
+                const f2 tx = f2{fminf(fminf(tfx.x, tfy.x), tfz.x), fminf(fminf(tfx.y, tfy.y), tfz.y)} * f2{1.00001f, 1.00001f};
+                bool h0 = te.x <= tx.x, h1 = te.y <= tx.y;
+                if (!kAnyHit) { h0 = h0 && te.x <= tcull; h1 = h1 && te.y <= tcull; }
+                tc[k] = h0 ? fminf(te.x, FLT_MAX) : INFINITY;
+                tc[k + 1] = h1 ? fminf(te.y, FLT_MAX) : INFINITY;
+            }
+#else
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const float tnx = q_decode(cnx, kx, wnx, k), tfx = q_decode(cfx, kx, wfx, k);
@@ -467,6 +495,7 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
                 if (!kAnyHit) h = h && te <= tcull;
                 tc[k] = h ? fminf(te, FLT_MAX) : INFINITY;   // hits sort before misses
             }
+#endif
             if (!kAnyHit || kSortAnyHit) {
                 // (the network costs ~25 VALU; nodes where one child or none is wanted skip it)
                 const int nh = (tc[0] != INFINITY) + (tc[1] != INFINITY) + (tc[2] != INFINITY) + (tc[3] != INFINITY);
@@ -543,6 +572,303 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
     if (st) { RT_STAMP(s0); st->v[5] += s0 - q0; }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// "While-while" four-wide traversal (RT_WHILE_WHILE, default; Aila & Laine 2009's speculative form):
+// a lane that reaches a leaf postpones it and keeps visiting nodes until every lane of the wave
+// holds a leaf (or has finished), then the wave tests leaves together. Node and triangle
+// arithmetic are bvh4_query's; only the interleaving of node visits and leaf tests changes, so
+// the lexicographic minimum and the any-hit verdict are the same.
+// ---------------------------------------------------------------------------------------------
+#ifndef RT_WHILE_WHILE
+#define RT_WHILE_WHILE 1   // measured 5% faster C4 frame, 4% C5, than bvh4_query (0; the RT_STAMPS probe uses that one)
+#endif
+#ifndef RT_WW_SLACK
+#define RT_WW_SLACK 0   // measured: 0 best (4: +5%, 12: +10%, 24: +20% frame time)
+#endif
+#ifndef RT_WW_CURSOR
+#define RT_WW_CURSOR 1   // measured 2% faster C4 and C5 than whole leaves per iteration
+#endif
+#ifndef RT_WW_LEAVES
+#define RT_WW_LEAVES 1
+#endif
+constexpr int32_t kDoneRef = kBvhEmpty;   // "no ref": a count-0 leaf is never a wanted child
+
+struct Ray4 {
+    V3 o, inv;
+    float pnx, pny, pnz, tcull;
+    bool nx, ny, nz;
+};
+
+// One node visit: the wanted children by entry distance, the far ones pushed; returns the next ref
+// (the nearest wanted child, else the stack top, else kDoneRef).
+template <bool kAnyHit>
+__device__ __forceinline__ int32_t node4_next(const Ray4 &R, uint4 a, uint4 b, uint4 c, uint4 d, const LaneStack &stack,
+                                              int &sp) {
+    const V3 o = R.o, inv = R.inv;
+    const float dx = __uint_as_float(a.x) - o.x, dy = __uint_as_float(a.y) - o.y, dz = __uint_as_float(a.z) - o.z;
+    const float kx = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w)) + 127) << 23) * inv.x;
+    const float ky = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 8)) + 127) << 23) * inv.y;
+    const float kz = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 16)) + 127) << 23) * inv.z;
+    const float cnx = (dx + R.pnx) * inv.x, cfx = (dx - R.pnx) * inv.x;
+    const float cny = (dy + R.pny) * inv.y, cfy = (dy - R.pny) * inv.y;
+    const float cnz = (dz + R.pnz) * inv.z, cfz = (dz - R.pnz) * inv.z;
+    const uint32_t wnx = R.nx ? b.w : b.x, wfx = R.nx ? b.x : b.w;
+    const uint32_t wny = R.ny ? c.x : b.y, wfy = R.ny ? b.y : c.x;
+    const uint32_t wnz = R.nz ? c.y : b.z, wfz = R.nz ? b.z : c.y;
+    int32_t rc[4] = {static_cast<int32_t>(c.z), static_cast<int32_t>(c.w), static_cast<int32_t>(d.x),
+                     static_cast<int32_t>(d.y)};
+    float tc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float tnx = q_decode(cnx, kx, wnx, k), tfx = q_decode(cfx, kx, wfx, k);
+        const float tny = q_decode(cny, ky, wny, k), tfy = q_decode(cfy, ky, wfy, k);
+        const float tnz = q_decode(cnz, kz, wnz, k), tfz = q_decode(cfz, kz, wfz, k);
+        const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
+        const float tx = fminf(fminf(tfx, tfy), tfz);
+        bool h = te <= tx * 1.00001f;
+        if (!kAnyHit) h = h && te <= R.tcull;
+        tc[k] = h ? fminf(te, FLT_MAX) : INFINITY;
+    }
+    if (!kAnyHit || kSortAnyHit) {
+        const int nh = (tc[0] != INFINITY) + (tc[1] != INFINITY) + (tc[2] != INFINITY) + (tc[3] != INFINITY);
+        if (nh > 1) {
+            cswap(tc[0], rc[0], tc[1], rc[1]);
+            cswap(tc[2], rc[2], tc[3], rc[3]);
+            cswap(tc[0], rc[0], tc[2], rc[2]);
+            cswap(tc[1], rc[1], tc[3], rc[3]);
+            cswap(tc[1], rc[1], tc[2], rc[2]);
+        } else if (nh == 1) {
+            const int32_t one = tc[0] != INFINITY ? rc[0] : tc[1] != INFINITY ? rc[1] : tc[2] != INFINITY ? rc[2] : rc[3];
+            rc[0] = one;
+            tc[0] = 0.0f;
+            tc[1] = tc[2] = tc[3] = INFINITY;
+        }
+        if (tc[3] != INFINITY) stack.push(sp, rc[3]);
+        if (tc[2] != INFINITY) stack.push(sp, rc[2]);
+        if (tc[1] != INFINITY) stack.push(sp, rc[1]);
+        if (tc[0] != INFINITY) return rc[0];
+    } else {
+        int32_t nxt = kDoneRef;
+        bool have = false;
+#pragma unroll
+        for (int k = 3; k >= 0; --k) {
+            if (tc[k] != INFINITY) {
+                if (have) stack.push(sp, nxt);
+                nxt = rc[k];
+                have = true;
+            }
+        }
+        if (have) return nxt;
+    }
+    return sp ? stack.pop(sp) : kDoneRef;
+}
+
+template <bool kAnyHit>
+__device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, bool active, int &bidx, V3 &bI,
+                                              const LaneStack &stack, unsigned &tests, unsigned &visits) {
+    float best = FLT_MAX;
+    bool done = !active;
+    test_always<kAnyHit>(sc, o, dir, best, bidx, bI, done);
+    if (!active || (kAnyHit && done)) return;
+    Ray4 R;   // bvh4_query's per-ray constants
+    V3 inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+    constexpr float kInvMax = 0x1p100f;
+    if (!(fabsf(inv.x) <= kInvMax)) inv.x = copysignf(kInvMax, dir.x);
+    if (!(fabsf(inv.y) <= kInvMax)) inv.y = copysignf(kInvMax, dir.y);
+    if (!(fabsf(inv.z) <= kInvMax)) inv.z = copysignf(kInvMax, dir.z);
+    const float pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
+    const float dlen = sqrtf(dot(dir, dir));
+    R.o = o;
+    R.inv = inv;
+    R.nx = inv.x < 0; R.ny = inv.y < 0; R.nz = inv.z < 0;
+    R.pnx = R.nx ? pad : -pad; R.pny = R.ny ? pad : -pad; R.pnz = R.nz ? pad : -pad;
+    R.tcull = INFINITY;
+    int sp = 0;
+    int32_t node = 0;          // inner node to visit, a leaf ref, or kDoneRef
+    int32_t leaf = kDoneRef;   // the postponed leaf
+    int32_t leaf2 = kDoneRef;  // a second one (RT_WW_LEAVES 2)
+    while (true) {
+        while (node >= 0) {
+            ++visits;
+            uint4 a, b, c, d;
+            load_node4(stack, sc.nodes4, node, a, b, c, d);
+            node = node4_next<kAnyHit>(R, a, b, c, d, stack, sp);
+            if (node < 0 && node != kDoneRef && leaf == kDoneRef) {   // postpone it, keep walking
+                leaf = node;
+                node = sp ? stack.pop(sp) : kDoneRef;
+            }
+            if (RT_WW_LEAVES > 1 && node < 0 && node != kDoneRef && leaf2 == kDoneRef) {   // and a second one
+                leaf2 = node;
+                node = sp ? stack.pop(sp) : kDoneRef;
+            }
+            // every lane still walking holds a leaf (RT_WW_SLACK: or all but that many)
+            if (RT_WW_LEAVES > 1 ? __all(leaf2 != kDoneRef)
+                                 : RT_WW_SLACK == 0 ? __all(leaf != kDoneRef) : __popcll(__ballot(leaf == kDoneRef)) <= RT_WW_SLACK)
+                break;
+        }
+        while (leaf != kDoneRef) {
+            const uint32_t u = static_cast<uint32_t>(leaf);
+            const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
+            const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
+            if (RT_WW_CURSOR) {
+                // one triangle per iteration: the ref is the cursor (first + 1, count - 1), so a lane
+                // whose leaf ends goes on to its next leaf while the others test their next triangle
+                const TriRec T = sc.leaf_recs[first];
+                test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first]), o, dir, best, bidx, bI, done);
+                ++tests;
+                if (kAnyHit && done) { node = kDoneRef; leaf2 = kDoneRef; break; }
+                if (cnt > 1) {
+                    leaf = static_cast<int32_t>(u + 1u - (1u << kBvhCountShift));
+                    continue;
+                }
+            } else {
+                test_leaf<kAnyHit>(sc, first, cnt, o, dir, best, bidx, bI, done);
+                tests += static_cast<unsigned>(cnt);
+                if (kAnyHit && done) { node = kDoneRef; leaf2 = kDoneRef; break; }
+            }
+            if (!kAnyHit && best < FLT_MAX) R.tcull = (best * 1.00002f + pad) / dlen * 1.00001f;
+            leaf = kDoneRef;
+            if (RT_WW_LEAVES > 1 && leaf2 != kDoneRef) {
+                leaf = leaf2;
+                leaf2 = kDoneRef;
+            } else if (node < 0 && node != kDoneRef) {
+                leaf = node;
+                node = sp ? stack.pop(sp) : kDoneRef;
+            }
+        }
+        if (node == kDoneRef) break;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Two shadow queries of one hit in one walk (isShadow for lights l and l+1, raytracing.cpp:241-261):
+// both rays start at the same point, so they share the node frame offset and the pad; each keeps
+// its own slab arithmetic (bvh4_query's, per ray), its own cull distance and verdict. A child is
+// visited when either ray wants it, so each ray reaches every leaf its own walk would (and tests
+// a superset of its triangles, which cannot change a lexicographic minimum or an any-hit
+// verdict); a ray that is finished (any-hit accepted) wants nothing. The node and triangle
+// records are fetched once for both rays: half the dependent loads of two separate walks.
+// ---------------------------------------------------------------------------------------------
+#ifndef RT_SHADOW_PAIRS
+#define RT_SHADOW_PAIRS 0   // measured slower on C4 (1.04 vs 0.88 ms) and C5: the second ray's slab and
+                            // triangle arithmetic costs more than the shared fetches save
+#endif
+struct PairRay {
+    V3 dir, inv;
+    float dlen, tcull, best;
+    int bidx;
+    bool done;
+};
+
+__device__ __forceinline__ void pair_ray_init(PairRay &r, V3 dir) {
+    r.dir = dir;
+    V3 inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+    constexpr float kInvMax = 0x1p100f;   // see bvh4_query
+    if (!(fabsf(inv.x) <= kInvMax)) inv.x = copysignf(kInvMax, dir.x);
+    if (!(fabsf(inv.y) <= kInvMax)) inv.y = copysignf(kInvMax, dir.y);
+    if (!(fabsf(inv.z) <= kInvMax)) inv.z = copysignf(kInvMax, dir.z);
+    r.inv = inv;
+    r.dlen = sqrtf(dot(dir, dir));
+    r.tcull = INFINITY;
+}
+
+// Entry distances of the four children for one ray (INFINITY: not wanted), bvh4_query's arithmetic.
+template <bool kAnyHit>
+__device__ __forceinline__ void pair_children(const PairRay &r, float pad, float dx, float dy, float dz, uint4 a, uint4 b,
+                                              uint4 c, float (&tc)[4]) {
+    const V3 inv = r.inv;
+    const bool nx = inv.x < 0, ny = inv.y < 0, nz = inv.z < 0;
+    const float pnx = nx ? pad : -pad, pny = ny ? pad : -pad, pnz = nz ? pad : -pad;
+    const float kx = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w)) + 127) << 23) * inv.x;
+    const float ky = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 8)) + 127) << 23) * inv.y;
+    const float kz = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 16)) + 127) << 23) * inv.z;
+    const float cnx = (dx + pnx) * inv.x, cfx = (dx - pnx) * inv.x;
+    const float cny = (dy + pny) * inv.y, cfy = (dy - pny) * inv.y;
+    const float cnz = (dz + pnz) * inv.z, cfz = (dz - pnz) * inv.z;
+    const uint32_t wnx = nx ? b.w : b.x, wfx = nx ? b.x : b.w;
+    const uint32_t wny = ny ? c.x : b.y, wfy = ny ? b.y : c.x;
+    const uint32_t wnz = nz ? c.y : b.z, wfz = nz ? b.z : c.y;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float tnx = q_decode(cnx, kx, wnx, k), tfx = q_decode(cfx, kx, wfx, k);
+        const float tny = q_decode(cny, ky, wny, k), tfy = q_decode(cfy, ky, wfy, k);
+        const float tnz = q_decode(cnz, kz, wnz, k), tfz = q_decode(cfz, kz, wfz, k);
+        const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
+        const float tx = fminf(fminf(tfx, tfy), tfz);
+        bool h = te <= tx * 1.00001f && !r.done;
+        if (!kAnyHit) h = h && te <= r.tcull;
+        tc[k] = h ? fminf(te, FLT_MAX) : INFINITY;
+    }
+}
+
+template <bool kAnyHit>
+__device__ __forceinline__ void bvh4_query_pair(const DevScene &sc, V3 o, PairRay &r0, PairRay &r1,
+                                                const LaneStack &stack, unsigned &tests, unsigned &visits) {
+    V3 dummy = mk(0, 0, 0);
+    test_always<kAnyHit>(sc, o, r0.dir, r0.best, r0.bidx, dummy, r0.done);
+    test_always<kAnyHit>(sc, o, r1.dir, r1.best, r1.bidx, dummy, r1.done);
+    if (kAnyHit && r0.done && r1.done) return;
+    const float pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
+    int sp = 0;
+    int32_t ref = 0;
+    while (true) {
+        if (ref >= 0) {
+            ++visits;
+            uint4 a, b, c, d;
+            load_node4(stack, sc.nodes4, ref, a, b, c, d);
+            const float dx = __uint_as_float(a.x) - o.x, dy = __uint_as_float(a.y) - o.y, dz = __uint_as_float(a.z) - o.z;
+            float t0[4], t1[4];
+            pair_children<kAnyHit>(r0, pad, dx, dy, dz, a, b, c, t0);
+            pair_children<kAnyHit>(r1, pad, dx, dy, dz, a, b, c, t1);
+            int32_t rc[4] = {static_cast<int32_t>(c.z), static_cast<int32_t>(c.w), static_cast<int32_t>(d.x),
+                             static_cast<int32_t>(d.y)};
+            float tc[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) tc[k] = fminf(t0[k], t1[k]);   // wanted by either ray
+            const int nh = (tc[0] != INFINITY) + (tc[1] != INFINITY) + (tc[2] != INFINITY) + (tc[3] != INFINITY);
+            if (nh > 1) {
+                cswap(tc[0], rc[0], tc[1], rc[1]);
+                cswap(tc[2], rc[2], tc[3], rc[3]);
+                cswap(tc[0], rc[0], tc[2], rc[2]);
+                cswap(tc[1], rc[1], tc[3], rc[3]);
+                cswap(tc[1], rc[1], tc[2], rc[2]);
+            } else if (nh == 1) {
+                const int32_t one = tc[0] != INFINITY ? rc[0] : tc[1] != INFINITY ? rc[1] : tc[2] != INFINITY ? rc[2] : rc[3];
+                rc[0] = one;
+                tc[0] = 0.0f;
+                tc[1] = tc[2] = tc[3] = INFINITY;
+            }
+            if (tc[3] != INFINITY) stack.push(sp, rc[3]);
+            if (tc[2] != INFINITY) stack.push(sp, rc[2]);
+            if (tc[1] != INFINITY) stack.push(sp, rc[1]);
+            if (tc[0] != INFINITY) {
+                ref = rc[0];
+            } else {
+                if (sp == 0) break;
+                ref = stack.pop(sp);
+            }
+        } else {
+            const uint32_t u = static_cast<uint32_t>(ref);
+            const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
+            const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
+            for (int k = 0; k < cnt; ++k) {
+                const TriRec T = sc.leaf_recs[first + k];
+                const int t = static_cast<int>(sc.leaf_idx[first + k]);
+                test_triangle<kAnyHit, true>(T, t, o, r0.dir, r0.best, r0.bidx, dummy, r0.done);
+                test_triangle<kAnyHit, true>(T, t, o, r1.dir, r1.best, r1.bidx, dummy, r1.done);
+            }
+            if (!kAnyHit) {
+                if (r0.best < FLT_MAX) r0.tcull = (r0.best * 1.00002f + pad) / r0.dlen * 1.00001f;
+                if (r1.best < FLT_MAX) r1.tcull = (r1.best * 1.00002f + pad) / r1.dlen * 1.00001f;
+            }
+            tests += static_cast<unsigned>(cnt);
+            if (kAnyHit && r0.done && r1.done) break;
+            if (sp == 0) break;
+            ref = stack.pop(sp);
+        }
+    }
+}
 
 // ---------------------------------------------------------------------------------------------
 // Wave-coherent four-wide traversal (W = 5): the 64 lanes of a wave walk ONE path through the
@@ -662,6 +988,7 @@ __device__ __forceinline__ void bvh_query_w(const DevScene &sc, const Bvh4Node *
                                             Stamps *st = nullptr) {
     if (W == 5) wave_query<kAnyHit>(sc, n4, lrec, lidx, o, dir, active, bidx, bI, lds + (threadIdx.x >> 6) * sc.bvh4_stack,
                                     tests, visits);
+    else if (W == 4 && RT_WHILE_WHILE && !st) bvh4_query_ww<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
     else if (W == 4) bvh4_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits, st);
     else bvh_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
 }
@@ -1318,7 +1645,21 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
             if (shadows) {
                 atomicAdd(&s_sh[step], p.n_lights);
                 const V3 so = mk(bI.x + 0.1f, bI.y + 0.1f, bI.z + 0.1f);                // :248
-                for (int l = 0; l < p.n_lights; ++l) {
+                int l = 0;
+                if (W == 4 && RT_SHADOW_PAIRS) {   // two lights per walk (bvh4_query_pair)
+                    for (; l + 1 < p.n_lights; l += 2) {
+                        PairRay r0, r1;
+                        r0.best = r1.best = FLT_MAX;
+                        r0.bidx = r1.bidx = -1;
+                        r0.done = r1.done = false;
+                        pair_ray_init(r0, mk(p.lights[l][0] - so.x, p.lights[l][1] - so.y, p.lights[l][2] - so.z));
+                        pair_ray_init(r1, mk(p.lights[l + 1][0] - so.x, p.lights[l + 1][1] - so.y, p.lights[l + 1][2] - so.z));
+                        bvh4_query_pair<kAnyHit>(sc, so, r0, r1, stack, ws.tests, ws.visits);
+                        if (r0.bidx >= 0 && !sc.mats[sc.tri_mat[r0.bidx]].transparent) mask |= 1u << l;         // :253-257
+                        if (r1.bidx >= 0 && !sc.mats[sc.tri_mat[r1.bidx]].transparent) mask |= 1u << (l + 1);
+                    }
+                }
+                for (; l < p.n_lights; ++l) {
                     int sidx = -1;
                     V3 sI = mk(0, 0, 0);
                     const V3 sd = mk(p.lights[l][0] - so.x, p.lights[l][1] - so.y, p.lights[l][2] - so.z);
