@@ -73,8 +73,8 @@ def workload_scene(spec, workdir):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mode", choices=("weak", "strong"), default="weak")
     ap.add_argument("--cpu-sample-every", type=int, default=96, help="CPU baseline: every k-th tile")
     ap.add_argument("--cpu-threads", type=int, default=16)

@@ -210,14 +210,11 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
 #define RT_TUNE_CHAIN_FROM 9     /* chain steps from this one on run in one launch, each lane carrying
                                     its ray through closest-hit, shadows and shade (default 0;
                                     >= max_lvl + 1: every step its own launches) */
-#define RT_TUNE_CHAIN_KERNEL 10  /* 0 (default): each lane of the chain launch runs its queries phase by
-                                    phase (closest, shadows, shade); 1: every lane stays busy, one
-                                    traversal step per iteration, and lanes whose query ended are
-                                    refilled (measured slower: lanes drift apart, L1 misses x3.7) */
 #define RT_TUNE_TOP_NODES 13     /* four-wide nodes of the tree's top levels (breadth-first, the first
                                     ones in the node array) each block reads from an LDS copy (0-85) */
-#define RT_TUNE_CHAIN_SPLIT 12   /* query distribution of the phased chain launch, as RT_TUNE_XCD_SPLIT */
-#define RT_TUNE_REFILL 11        /* chain kernel 1: lanes of a wave waiting before it advances them (1-64) */
+#define RT_TUNE_CHAIN_SPLIT 12   /* query distribution of the chain launch: as RT_TUNE_XCD_SPLIT, or 3: 64-query
+                                    chunks dealt round-robin to the XCDs and taken dynamically within
+                                    each (+4: reversed order, diagnostic) */
 #define RT_TUNE_PIPE_BATCHES 6     /* split a call into at least pipes x this many batches */
 #define RT_TUNE_PIPE_PRIORITY 7    /* 1 (default): pipelines after the first run at lower stream priority */
 #define RT_TUNE_SHADOW_VIRTUAL 5   /* bit k: step k's shadow rays are read from its hits directly

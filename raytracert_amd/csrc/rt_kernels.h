@@ -80,8 +80,6 @@ struct DevScene {
     int32_t xcd_split;              // RT_TUNE_XCD_SPLIT
     int32_t bvh_grid;               // RT_TUNE_BVH_GRID
     unsigned long long *work;       // BVH kernels' work counters: [0, kWorkFields) closest-hit, then shadow
-    int32_t chain_kernel;           // RT_TUNE_CHAIN_KERNEL: 0 phased per-lane chain, 1 per-lane refill
-    int32_t refill;                 // RT_TUNE_REFILL: waiting lanes before a refill wave advances them
     int32_t chain_split;            // RT_TUNE_CHAIN_SPLIT: query distribution of k_chain (as xcd_split)
     int32_t top_nodes;              // RT_TUNE_TOP_NODES: four-wide nodes [0, top_nodes) read from an LDS copy
 };

@@ -199,13 +199,13 @@ struct RayBox { V3 o, inv; float pad, dlen; };
 // entries in a global overflow area ([entry - cap][global lane], coalesced). Trees deeper than
 // the LDS part are rare, so a small LDS part keeps occupancy high at no cost in the common case.
 struct LaneStack {
-    int32_t (*lds)[kBvhBlock];
+    int32_t *lds;       // [entry][width lanes]
     int32_t *ovf;
-    int cap, stride, gl;
+    int cap, stride, gl, width;
     const uint4 *top;   // LDS copy of the four-wide node array's first ntop nodes (the top levels)
     int ntop;
     __device__ __forceinline__ void push(int &sp, int32_t v) const {
-        if (sp < cap) lds[sp][threadIdx.x] = v;
+        if (sp < cap) lds[sp * width + static_cast<int>(threadIdx.x)] = v;
         else ovf[static_cast<size_t>(sp - cap) * stride + gl] = v;
         ++sp;
     }
@@ -213,7 +213,7 @@ struct LaneStack {
         --sp;
         // the LDS read is unconditional so the two reads stay a ds_read and a global load (a
         // select between the two pointers would become a slower flat load)
-        int32_t v = lds[min(sp, cap - 1)][threadIdx.x];
+        int32_t v = lds[min(sp, cap - 1) * width + static_cast<int>(threadIdx.x)];
         if (sp >= cap) v = ovf[static_cast<size_t>(sp - cap) * stride + gl];
         return v;
     }
@@ -221,14 +221,16 @@ struct LaneStack {
 
 // Dynamic LDS of the per-lane BVH kernels: [lds_stack entries][128 lanes] of stack, then the top
 // nodes. Every thread of the block must call this before its first query (barrier).
+template <int B = kBvhBlock>
 __device__ __forceinline__ LaneStack lane_stack(const DevScene &sc, int32_t *lds) {
     LaneStack st;
-    st.lds = reinterpret_cast<int32_t (*)[kBvhBlock]>(lds);
+    st.lds = lds;
+    st.width = B;
     st.ovf = sc.stack_ovf;
     st.cap = sc.lds_stack;
-    st.stride = static_cast<int>(gridDim.x) * kBvhBlock;
-    st.gl = static_cast<int>(blockIdx.x) * kBvhBlock + static_cast<int>(threadIdx.x);
-    uint4 *top = reinterpret_cast<uint4 *>(lds + static_cast<size_t>(max(sc.lds_stack, 1)) * kBvhBlock);
+    st.stride = static_cast<int>(gridDim.x) * B;
+    st.gl = static_cast<int>(blockIdx.x) * B + static_cast<int>(threadIdx.x);
+    uint4 *top = reinterpret_cast<uint4 *>(lds + static_cast<size_t>(max(sc.lds_stack, 1)) * B);
     st.top = top;
     st.ntop = sc.top_nodes;
     if (sc.top_nodes > 0) {
@@ -1595,16 +1597,63 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(const DevScene sc, const 
     }
 }
 
+constexpr int kChainSteps = 256;   // max_lvl <= 254
+#ifndef RT_CHAIN_WPE
+#define RT_CHAIN_WPE 6   // measured: 6 (80 VGPRs, 36 B spill) beats 5 (92, none) and 7
+#endif
+
+// One chain step of one sample (trace, raytracing.cpp:381-406): the closest-hit query, isShadow
+// per light (:241-261), shade (:335-368). Returns the secondary ray (state kChildTrace) or the end
+// of the chain. Shadow-ray statistics are counted per block in s_sh.
+template <bool kAnyHit, int W, bool kCount>
+__device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeParams &p, const DevWork &w, int step,
+                                                int sample, V3 org, V3 dst, int lvl, const LaneStack &stack,
+                                                int32_t *lds_stack, const Bvh4Node *__restrict__ n4,
+                                                const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx,
+                                                int *s_sh, WorkTally<kCount> &wc, WorkTally<kCount> &ws) {
+    Secondary none;
+    none.state = kChildNone;
+    int bidx = -1;
+    V3 bI = mk(0, 0, 0);
+    bvh_query_w<false, W>(sc, n4, lrec, lidx, lds_stack, org, sub(dst, org), true, bidx, bI, stack, wc.tests, wc.visits);
+    if (bidx >= sc.nt) { w.counters[kErrorSlot] = 1; bidx = -1; }
+    if (bidx < 0) { shade_miss(w, step, sample); return none; }
+    uint32_t mask = 0;   // isShadow per light (:241-261)
+    const bool shadows = (p.flags & RT_SHADOWS) && p.n_lights > 0;
+    if (shadows) {
+        atomicAdd(&s_sh[step], p.n_lights);
+        const V3 so = mk(bI.x + 0.1f, bI.y + 0.1f, bI.z + 0.1f);                // :248
+        int l = 0;
+        if (W == 4 && RT_SHADOW_PAIRS) {   // two lights per walk (bvh4_query_pair)
+            for (; l + 1 < p.n_lights; l += 2) {
+                PairRay r0, r1;
+                r0.best = r1.best = FLT_MAX;
+                r0.bidx = r1.bidx = -1;
+                r0.done = r1.done = false;
+                pair_ray_init(r0, mk(p.lights[l][0] - so.x, p.lights[l][1] - so.y, p.lights[l][2] - so.z));
+                pair_ray_init(r1, mk(p.lights[l + 1][0] - so.x, p.lights[l + 1][1] - so.y, p.lights[l + 1][2] - so.z));
+                bvh4_query_pair<kAnyHit>(sc, so, r0, r1, stack, ws.tests, ws.visits);
+                if (r0.bidx >= 0 && !sc.mats[sc.tri_mat[r0.bidx]].transparent) mask |= 1u << l;         // :253-257
+                if (r1.bidx >= 0 && !sc.mats[sc.tri_mat[r1.bidx]].transparent) mask |= 1u << (l + 1);
+            }
+        }
+        for (; l < p.n_lights; ++l) {
+            int sidx = -1;
+            V3 sI = mk(0, 0, 0);
+            const V3 sd = mk(p.lights[l][0] - so.x, p.lights[l][1] - so.y, p.lights[l][2] - so.z);
+            bvh_query_w<kAnyHit, W>(sc, n4, lrec, lidx, lds_stack, so, sd, true, sidx, sI, stack, ws.tests, ws.visits);
+            if (sidx >= 0 && !sc.mats[sc.tri_mat[sidx]].transparent) mask |= 1u << l;   // :253-257
+        }
+    }
+    return shade_hit(sc, p, w, step, sample, sub(dst, org), lvl, bidx, bI, [&](int l) { return ((mask >> l) & 1u) != 0; });
+}
+
 // Chain tail (RT_TUNE_CHAIN_FROM): the remaining steps of every query in Q_first, each lane
 // carrying its own ray through closest-hit, its shadow rays and shade until its chain ends. With
 // no launch boundary between steps, a lane's next step does not wait for the slowest wave of the
 // current one, which is what the thin last steps spend their time on. The per-ray arithmetic is
 // the per-step kernels' own (the same functions). Query counts per step (ray statistics) are
 // summed per block in LDS and added to the step counters once at the end.
-constexpr int kChainSteps = 256;   // max_lvl <= 254
-#ifndef RT_CHAIN_WPE
-#define RT_CHAIN_WPE 6   // measured: 6 (80 VGPRs, 36 B spill) beats 5 (92, none) and 7
-#endif
 template <int W, bool kAnyHit, bool kCount>
 __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CHAIN_WPE))) void k_chain(
     const DevScene sc, const ShadeParams p, DevWork w, int first, const Bvh4Node *__restrict__ n4,
@@ -1614,7 +1663,6 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
     for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) { s_q[i] = 0; s_sh[i] = 0; }
     __syncthreads();
     const LaneStack stack = lane_stack(sc, lds_stack);
-    const bool shadows = (p.flags & RT_SHADOWS) && p.n_lights > 0;
     WorkTally<kCount> wc, ws;   // closest-hit and shadow work (totals only: lanes diverge here)
 #ifdef RT_WAVE_TIMES   // diagnostic build: each wave's start / end clock (100 MHz) and query count
     unsigned long long *wt_out = sc.work ? sc.work + 2 * kWorkFields + 3 * ((blockIdx.x * kBvhBlock + threadIdx.x) >> 6) : nullptr;
@@ -1636,39 +1684,8 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
         V3 org = mk(qo.x, qo.y, qo.z), dst = mk(qd.x, qd.y, qd.z);
         for (int step = first; step < kChainSteps; ++step) {
             if (step > first) atomicAdd(&s_q[step], 1);
-            int bidx = -1;
-            V3 bI = mk(0, 0, 0);
-            bvh_query_w<false, W>(sc, n4, lrec, lidx, lds_stack, org, sub(dst, org), true, bidx, bI, stack, wc.tests, wc.visits);
-            if (bidx >= sc.nt) { w.counters[kErrorSlot] = 1; bidx = -1; }
-            if (bidx < 0) { shade_miss(w, step, sample); break; }
-            uint32_t mask = 0;   // isShadow per light (:241-261)
-            if (shadows) {
-                atomicAdd(&s_sh[step], p.n_lights);
-                const V3 so = mk(bI.x + 0.1f, bI.y + 0.1f, bI.z + 0.1f);                // :248
-                int l = 0;
-                if (W == 4 && RT_SHADOW_PAIRS) {   // two lights per walk (bvh4_query_pair)
-                    for (; l + 1 < p.n_lights; l += 2) {
-                        PairRay r0, r1;
-                        r0.best = r1.best = FLT_MAX;
-                        r0.bidx = r1.bidx = -1;
-                        r0.done = r1.done = false;
-                        pair_ray_init(r0, mk(p.lights[l][0] - so.x, p.lights[l][1] - so.y, p.lights[l][2] - so.z));
-                        pair_ray_init(r1, mk(p.lights[l + 1][0] - so.x, p.lights[l + 1][1] - so.y, p.lights[l + 1][2] - so.z));
-                        bvh4_query_pair<kAnyHit>(sc, so, r0, r1, stack, ws.tests, ws.visits);
-                        if (r0.bidx >= 0 && !sc.mats[sc.tri_mat[r0.bidx]].transparent) mask |= 1u << l;         // :253-257
-                        if (r1.bidx >= 0 && !sc.mats[sc.tri_mat[r1.bidx]].transparent) mask |= 1u << (l + 1);
-                    }
-                }
-                for (; l < p.n_lights; ++l) {
-                    int sidx = -1;
-                    V3 sI = mk(0, 0, 0);
-                    const V3 sd = mk(p.lights[l][0] - so.x, p.lights[l][1] - so.y, p.lights[l][2] - so.z);
-                    bvh_query_w<kAnyHit, W>(sc, n4, lrec, lidx, lds_stack, so, sd, true, sidx, sI, stack, ws.tests, ws.visits);
-                    if (sidx >= 0 && !sc.mats[sc.tri_mat[sidx]].transparent) mask |= 1u << l;   // :253-257
-                }
-            }
-            const Secondary sec = shade_hit(sc, p, w, step, sample, sub(dst, org), lvl, bidx, bI,
-                                            [&](int l) { return ((mask >> l) & 1u) != 0; });
+            const Secondary sec = chain_step<kAnyHit, W>(sc, p, w, step, sample, org, dst, lvl, stack, lds_stack, n4, lrec,
+                                                         lidx, s_sh, wc, ws);
             if (sec.state != kChildTrace) break;
             org = sec.org;
             dst = sec.dst;
@@ -1685,291 +1702,6 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
         wt_out[2] = wt_q | (static_cast<unsigned long long>(hwid) << 32) | (static_cast<unsigned long long>(xcc & 0xF) << 60);
     }
 #endif
-    wc.flush(sc.work);
-    ws.flush(sc.work ? sc.work + kWorkFields : nullptr);
-    __syncthreads();
-    for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) {
-        if (s_q[i]) atomicAdd(&w.counters[i], s_q[i]);
-        if (s_sh[i]) atomicAdd(&w.counters[kMaxStepsCounters + i], s_sh[i]);
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Chain with per-lane refill (RT_TUNE_CHAIN_KERNEL 1, the default). k_chain runs a lane's
-// closest-hit query, then its shadow queries, then shade, each phase to the end: a wave takes as
-// long as its slowest lane in every phase, and lanes whose chain ended idle until the whole wave's
-// 64 samples are done. Here every lane is a small state machine over one query at a time, and
-// each loop iteration is ONE traversal step of whatever query a lane holds: a four-wide node
-// visit or one triangle test. Node records and triangle records are both 64 B, so the step
-// issues one 64-B load per lane whichever it is, and the wave pays one memory latency per
-// iteration. Lanes whose query ended wait until `refill` of them are waiting (or none is
-// traversing); the wave then advances them together: record the verdict, start the next shadow
-// query, shade, start the next step's closest-hit query, or take a new sample. The per-query
-// arithmetic is bvh4_query's (node decode, cull, order) and test_triangle's, so every query's
-// result is the same; only the interleaving differs.
-// ---------------------------------------------------------------------------------------------
-struct Trav {
-    V3 o, dir, inv;
-    float pad, dlen, tcull, best;
-    int32_t ref;
-    int sp, bidx;
-    V3 bI;
-};
-
-// Start a query: the always list, then the root with bvh4_query's per-ray constants. Returns
-// false if the query is already finished (an any-hit query accepted an always-list triangle).
-__device__ __forceinline__ bool trav_begin(const DevScene &sc, Trav &t, V3 o, V3 dir, bool anyhit) {
-    t.o = o;
-    t.dir = dir;
-    t.best = FLT_MAX;
-    t.bidx = -1;
-    t.bI = mk(0, 0, 0);
-    bool done = false;
-    test_always<false>(sc, o, dir, t.best, t.bidx, t.bI, done);
-    if (anyhit && t.bidx >= 0) return false;
-    V3 inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
-    constexpr float kInvMax = 0x1p100f;   // see bvh4_query
-    if (!(fabsf(inv.x) <= kInvMax)) inv.x = copysignf(kInvMax, dir.x);
-    if (!(fabsf(inv.y) <= kInvMax)) inv.y = copysignf(kInvMax, dir.y);
-    if (!(fabsf(inv.z) <= kInvMax)) inv.z = copysignf(kInvMax, dir.z);
-    t.inv = inv;
-    t.pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
-    t.dlen = sqrtf(dot(dir, dir));
-    t.tcull = INFINITY;
-    t.sp = 0;
-    t.ref = 0;
-    return true;
-}
-
-enum : unsigned { kStepNode = 1u, kStepDone = 2u };
-
-// One traversal step. Returns kStepNode if it visited a node (else it tested a triangle), plus
-// kStepDone when the query is finished. Leaf refs double as the cursor: testing the leaf's first
-// triangle leaves ref = (first + 1, count - 1).
-__device__ __forceinline__ unsigned trav_step(const Bvh4Node *__restrict__ n4, const TriRec *__restrict__ lrec,
-                                              const uint32_t *__restrict__ lidx, const LaneStack &stack, Trav &t,
-                                              bool anyhit) {
-    const bool node = t.ref >= 0;
-    const uint32_t lf = static_cast<uint32_t>(t.ref) & ((1u << kBvhCountShift) - 1u);
-    uint4 a, b, c, d;
-    if (node && t.ref < stack.ntop) {
-        const uint4 *p = stack.top + 4 * t.ref;
-        a = p[0]; b = p[1]; c = p[2]; d = p[3];
-    } else {
-        const uint4 *ptr = node ? reinterpret_cast<const uint4 *>(n4 + t.ref) : reinterpret_cast<const uint4 *>(lrec + lf);
-        a = ptr[0]; b = ptr[1]; c = ptr[2]; d = ptr[3];
-    }
-    if (node) {
-        const V3 o = t.o, inv = t.inv;
-        const bool nx = inv.x < 0, ny = inv.y < 0, nz = inv.z < 0;
-        const float pnx = nx ? t.pad : -t.pad, pny = ny ? t.pad : -t.pad, pnz = nz ? t.pad : -t.pad;
-        const float dx = __uint_as_float(a.x) - o.x, dy = __uint_as_float(a.y) - o.y, dz = __uint_as_float(a.z) - o.z;
-        const float kx = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w)) + 127) << 23) * inv.x;
-        const float ky = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 8)) + 127) << 23) * inv.y;
-        const float kz = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 16)) + 127) << 23) * inv.z;
-        const float cnx = (dx + pnx) * inv.x, cfx = (dx - pnx) * inv.x;
-        const float cny = (dy + pny) * inv.y, cfy = (dy - pny) * inv.y;
-        const float cnz = (dz + pnz) * inv.z, cfz = (dz - pnz) * inv.z;
-        const uint32_t wnx = nx ? b.w : b.x, wfx = nx ? b.x : b.w;   // qlo / qhi words per axis
-        const uint32_t wny = ny ? c.x : b.y, wfy = ny ? b.y : c.x;
-        const uint32_t wnz = nz ? c.y : b.z, wfz = nz ? b.z : c.y;
-        int32_t rc[4] = {static_cast<int32_t>(c.z), static_cast<int32_t>(c.w), static_cast<int32_t>(d.x),
-                         static_cast<int32_t>(d.y)};
-        float tc[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float tnx = q_decode(cnx, kx, wnx, k), tfx = q_decode(cfx, kx, wfx, k);
-            const float tny = q_decode(cny, ky, wny, k), tfy = q_decode(cfy, ky, wfy, k);
-            const float tnz = q_decode(cnz, kz, wnz, k), tfz = q_decode(cfz, kz, wfz, k);
-            const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
-            const float tx = fminf(fminf(tfx, tfy), tfz);
-            const bool h = te <= tx * 1.00001f && te <= t.tcull;   // any-hit queries keep tcull = inf
-            tc[k] = h ? fminf(te, FLT_MAX) : INFINITY;
-        }
-        const int nh = (tc[0] != INFINITY) + (tc[1] != INFINITY) + (tc[2] != INFINITY) + (tc[3] != INFINITY);
-        if (nh > 1) {
-            cswap(tc[0], rc[0], tc[1], rc[1]);
-            cswap(tc[2], rc[2], tc[3], rc[3]);
-            cswap(tc[0], rc[0], tc[2], rc[2]);
-            cswap(tc[1], rc[1], tc[3], rc[3]);
-            cswap(tc[1], rc[1], tc[2], rc[2]);
-        } else if (nh == 1) {
-            const int32_t one = tc[0] != INFINITY ? rc[0] : tc[1] != INFINITY ? rc[1] : tc[2] != INFINITY ? rc[2] : rc[3];
-            rc[0] = one;
-            tc[0] = 0.0f;
-            tc[1] = tc[2] = tc[3] = INFINITY;
-        }
-        if (tc[3] != INFINITY) stack.push(t.sp, rc[3]);
-        if (tc[2] != INFINITY) stack.push(t.sp, rc[2]);
-        if (tc[1] != INFINITY) stack.push(t.sp, rc[1]);
-        if (tc[0] != INFINITY) {
-            t.ref = rc[0];
-            return kStepNode;
-        }
-        if (t.sp == 0) return kStepNode | kStepDone;
-        t.ref = stack.pop(t.sp);
-        return kStepNode;
-    }
-    TriRec T;
-    static_assert(sizeof(TriRec) == 64, "one 64-B record per step");
-    __builtin_memcpy(&T, &a, 16);
-    __builtin_memcpy(reinterpret_cast<char *>(&T) + 16, &b, 16);
-    __builtin_memcpy(reinterpret_cast<char *>(&T) + 32, &c, 16);
-    __builtin_memcpy(reinterpret_cast<char *>(&T) + 48, &d, 16);
-    bool done = false;
-    test_triangle<false, true>(T, static_cast<int>(lidx[lf]), t.o, t.dir, t.best, t.bidx, t.bI, done);
-    if (anyhit && t.bidx >= 0) return kStepDone;
-    if (((static_cast<uint32_t>(t.ref) >> kBvhCountShift) & kBvhCountMask) > 1u) {
-        t.ref = static_cast<int32_t>(static_cast<uint32_t>(t.ref) + 1u - (1u << kBvhCountShift));
-        return 0;
-    }
-    if (t.best < FLT_MAX) t.tcull = (t.best * 1.00002f + t.pad) / t.dlen * 1.00001f;   // (any-hit: best stays FLT_MAX)
-    if (t.sp == 0) return kStepDone;
-    t.ref = stack.pop(t.sp);
-    return 0;
-}
-
-#ifndef RT_PT_WPE
-#define RT_PT_WPE 6
-#endif
-constexpr int kSupplyChunk = 64;   // samples a wave claims per atomic
-
-template <bool kAnyHit, bool kCount>
-__global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_PT_WPE))) void k_chain_pt(
-    const DevScene sc, const ShadeParams p, DevWork w, int first, int32_t *__restrict__ supply,
-    const Bvh4Node *__restrict__ n4, const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx) {
-    extern __shared__ int32_t lds_stack[];
-    __shared__ int s_q[kChainSteps], s_sh[kChainSteps];
-    for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) { s_q[i] = 0; s_sh[i] = 0; }
-    __syncthreads();
-    const LaneStack stack = lane_stack(sc, lds_stack);
-    const bool shadows = (p.flags & RT_SHADOWS) && p.n_lights > 0;
-    const int nq = w.counters[first];
-    const float4 *__restrict__ q_org = w.q_org[first & 1];
-    const float4 *__restrict__ q_dst = w.q_dst[first & 1];
-    const int lane = __lane_id();
-    const unsigned long long below = (1ull << lane) - 1ull;
-    WorkTally<kCount> wc, ws;
-    // Sample supply: the queue is cut into one segment per XCD (screen order, so an XCD's waves
-    // share a compact part of the scene in its L2); a wave claims kSupplyChunk samples at a time
-    // from its own XCD's segment, then from the others in turn (wave-uniform state).
-    const int home = blockIdx.x % kXcds;
-    const int seg_len = (nq + kXcds - 1) / kXcds;
-    int seg_k = 0, sup = 0, sup_end = 0;
-    bool dry = nq <= 0;
-    // lane state: the chain (sample, step, level; the closest hit being shaded, its shadow mask)
-    // and the query in flight (light < 0: the step's closest-hit query, else shadow query `light`)
-    bool live = false, busy = false, pend = false;
-    int sample = 0, step = first, lvl = 0, light = -1, cidx = -1;
-    uint32_t mask = 0;
-    V3 cdir = mk(0, 0, 0), cI = mk(0, 0, 0), no = mk(0, 0, 0), nd = mk(0, 0, 0);
-    Trav t;
-    t.o = t.dir = t.inv = t.bI = mk(0, 0, 0);
-    t.pad = t.dlen = t.best = 0.0f;
-    t.tcull = INFINITY;
-    t.ref = 0;
-    t.sp = 0;
-    t.bidx = -1;
-    const int refill = sc.refill;
-    while (true) {
-        if (busy) {
-            const unsigned r = trav_step(n4, lrec, lidx, stack, t, kAnyHit && light >= 0);
-            if (kCount) {
-                if (light < 0) { if (r & kStepNode) ++wc.visits; else ++wc.tests; }
-                else { if (r & kStepNode) ++ws.visits; else ++ws.tests; }
-            }
-            if (r & kStepDone) busy = false;
-        }
-        const int waiting = __popcll(__ballot(!busy && (live || !dry)));
-        if (waiting < refill && __any(busy)) continue;
-        // ---- transitions of the lanes whose query ended ----
-        if (live && !busy) {
-            if (light < 0) {   // the step's closest-hit query (trace, raytracing.cpp:381-406)
-                int bidx = t.bidx;
-                if (bidx >= sc.nt) { w.counters[kErrorSlot] = 1; bidx = -1; }   // never expected
-                if (bidx < 0) {
-                    shade_miss(w, step, sample);
-                    live = false;
-                } else {
-                    cdir = t.dir;
-                    cidx = bidx;
-                    cI = t.bI;
-                    mask = 0;
-                    light = 0;
-                    if (shadows) atomicAdd(&s_sh[step], p.n_lights);
-                }
-            } else {           // isShadow for `light` (:241-261)
-                if (t.bidx >= 0 && !sc.mats[sc.tri_mat[t.bidx]].transparent) mask |= 1u << light;   // :253-257
-                ++light;
-            }
-            if (live) {
-                if (shadows && light < p.n_lights) {   // the next light's shadow query
-                    no = mk(cI.x + 0.1f, cI.y + 0.1f, cI.z + 0.1f);                              // :248
-                    nd = mk(p.lights[light][0] - no.x, p.lights[light][1] - no.y, p.lights[light][2] - no.z);
-                    pend = true;
-                } else {                                // every verdict known: shade
-                    const Secondary sec = shade_hit(sc, p, w, step, sample, cdir, lvl, cidx, cI,
-                                                    [&](int l) { return ((mask >> l) & 1u) != 0; });
-                    if (sec.state == kChildTrace && step + 1 < kChainSteps) {
-                        ++step;
-                        lvl = sec.lvl;
-                        light = -1;
-                        atomicAdd(&s_q[step], 1);
-                        no = sec.org;
-                        nd = sub(sec.dst, sec.org);
-                        pend = true;
-                    } else {
-                        live = false;
-                    }
-                }
-            }
-        }
-        // ---- lanes without a chain take the next samples, in lane order ----
-        while (!dry) {
-            const unsigned long long need = __ballot(!live);
-            if (!need) break;
-            if (sup >= sup_end) {
-                bool got = false;
-                while (seg_k < kXcds) {
-                    const int g = (home + seg_k) % kXcds;
-                    const int begin = min(nq, g * seg_len), end = min(nq, begin + seg_len);
-                    int b = 0;
-                    if (lane == 0) b = atomicAdd(&supply[g * kWqStride], kSupplyChunk);
-                    b = begin + __shfl(b, 0);
-                    if (b < end) {
-                        sup = b;
-                        sup_end = min(end, b + kSupplyChunk);
-                        got = true;
-                        break;
-                    }
-                    ++seg_k;
-                }
-                if (!got) { dry = true; break; }
-            }
-            const int take = min(__popcll(need), sup_end - sup);
-            const int rank = __popcll(need & below);
-            if (!live && rank < take) {
-                const int j = sup + rank;
-                const float4 qo = q_org[j], qd = q_dst[j];
-                if (as_int(qd.w) >= 0) {   // else outside the frame: no chain
-                    sample = as_int(qo.w);
-                    lvl = as_int(qd.w);
-                    step = first;
-                    light = -1;
-                    live = true;
-                    no = mk(qo.x, qo.y, qo.z);
-                    nd = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);
-                    pend = true;
-                }
-            }
-            sup += take;
-        }
-        if (pend) {
-            pend = false;
-            busy = trav_begin(sc, t, no, nd, kAnyHit && light >= 0);
-        }
-        if (dry && !__any(live)) break;
-    }
     wc.flush(sc.work);
     ws.flush(sc.work ? sc.work + kWorkFields : nullptr);
     __syncthreads();
@@ -2057,8 +1789,8 @@ void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevW
 }
 
 // LDS part of the traversal stack: lds_stack entries per lane (the rest overflows to global)
-inline size_t bvh_lds(const DevScene &s) {
-    return sizeof(int32_t) * kBvhBlock * static_cast<size_t>(std::max(s.lds_stack, 1)) + sizeof(Bvh4Node) * static_cast<size_t>(s.top_nodes);
+inline size_t bvh_lds(const DevScene &s, int lanes = kBvhBlock) {
+    return sizeof(int32_t) * lanes * static_cast<size_t>(std::max(s.lds_stack, 1)) + sizeof(Bvh4Node) * static_cast<size_t>(s.top_nodes);
 }
 // The LDS node cache holds four-wide nodes: off for the other tree kernels.
 inline DevScene for_width(DevScene s, int W) {
@@ -2167,13 +1899,6 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
     if (capacity <= 0) return;
     const bool wide = tree_variant(s0, -1) == 4;
     const DevScene s = for_width(s0, wide ? 4 : 2);
-    if (wide && s.chain_kernel == 1) {
-        auto k = s.any_transparent ? k_chain_pt<false, false> : k_chain_pt<true, false>;
-        if (s.work) k = s.any_transparent ? k_chain_pt<false, true> : k_chain_pt<true, true>;
-        hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, p, w, first,
-                           w.wq + (2 * first) * kWqSlot, s.nodes4, s.leaf_recs, s.leaf_idx);
-        return;
-    }
     auto k = wide ? (s.any_transparent ? k_chain<4, false, false> : k_chain<4, true, false>)
                   : (s.any_transparent ? k_chain<2, false, false> : k_chain<2, true, false>);
     if (s.work)

@@ -229,21 +229,20 @@ def test_render_accel_modes_match_golden(name, accel, workdir, gpu_available):
     _assert_image_close(u8, f32, gu8, gf32)
 
 
-@pytest.mark.parametrize("kernel,refill", [(0, 16), (1, 1), (1, 16), (1, 64)])
+@pytest.mark.parametrize("split", [0, 3])
 @pytest.mark.parametrize("chain_from", [0, 1, 2, 255])
 @pytest.mark.parametrize("name", ["F2_dodge_200x150", "F2b_shadow_test_160x120", "F3_spheres_128x72_pf2",
                                   "F4_refract_128x72"])
-def test_chain_tail_matches_golden(name, chain_from, kernel, refill, workdir, gpu_available):
+def test_chain_tail_matches_golden(name, chain_from, split, workdir, gpu_available):
     """The per-lane chain launch (RT_TUNE_CHAIN_FROM) from the first step, from the second, and
-    never, in both chain kernels (RT_TUNE_CHAIN_KERNEL: phased, and refill at several
-    thresholds): the golden frames and ray counts each time. F4 has transparent materials, so its
-    shadow rays take the closest-hit form; dodgeColorTest has always-list triangles."""
+    never, with grid-stride and dynamic (RT_TUNE_CHAIN_SPLIT 3) query distribution: the golden
+    frames and ray counts each time. F4 has transparent materials, so its shadow rays take the
+    closest-hit form; dodgeColorTest has always-list triangles."""
     entry = golden_index()[name]
     gu8, gf32 = golden(name)
     with R.Scene.load(scene_path(entry["scene"], workdir), device=0) as sc:
         sc.tune("chain_from", chain_from)
-        sc.tune("chain_kernel", kernel)
-        sc.tune("refill", refill)
+        sc.tune("chain_split", split)
         u8, f32, counts = sc.render(_params(entry), want_f32=True)
     assert [int(c) for c in counts] == entry["counts"]
     _assert_image_close(u8, f32, gu8, gf32)
@@ -256,14 +255,17 @@ def test_c4_full_frame_bvh_equals_brute_force(workdir, gpu_available):
     with R.Scene.load(scene_path("syn:C4", workdir), device=0) as sc:
         sc.set_accel("bvh")
         a, af, ac = sc.render(p, want_f32=True)
-        sc.tune("chain_kernel", 0)
+        sc.tune("chain_split", 3)
         a0, af0, ac0 = sc.render(p, want_f32=True)
-        sc.tune("chain_kernel", 1)
+        sc.tune("chain_split", 0)
+        sc.tune("top_nodes", 0)
+        a1, af1, ac1 = sc.render(p, want_f32=True)
+        sc.tune("top_nodes", 21)
         sc.tune("bvh_width", 2)
         a2, af2, ac2 = sc.render(p, want_f32=True)
         sc.set_accel("brute_force")
         b, bf, bc = sc.render(p, want_f32=True)
-    for x, xf, xc in ((a, af, ac), (a0, af0, ac0), (a2, af2, ac2)):
+    for x, xf, xc in ((a, af, ac), (a0, af0, ac0), (a1, af1, ac1), (a2, af2, ac2)):
         assert [int(v) for v in xc] == [int(v) for v in bc]
         assert np.array_equal(x, b)
         assert np.array_equal(xf.view(np.uint32), bf.view(np.uint32))
