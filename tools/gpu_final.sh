@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round-end evidence in one GPU call: parity tests, PMC passes of the bench's chain kernel
+# (summary also placed in profiles/ so the bench line's `traffic` uses it), the default bench line,
+# its rocprofv3 kernel stats, and the other BASELINE workloads. Every step time-limited; stops at
+# the first failure. Usage: tools/gpu_final.sh TAG
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+TAG=${1:-r01}
+mkdir -p gpurun_out/prof
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu_$TAG.log
+bash tools/gpu_pmc.sh $TAG > gpurun_out/pmc_$TAG.log 2>&1 || { echo "pmc failed"; tail -20 gpurun_out/pmc_$TAG.log; exit 1; }
+python3 tools/pmc_summary.py gpurun_out/pmc/$TAG gpurun_out/${TAG}_pmc.json > /dev/null && cp gpurun_out/${TAG}_pmc.json profiles/${TAG}_pmc.json
+timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "bench failed"; tail -30 gpurun_out/bench_$TAG.err; exit 1; }
+cat gpurun_out/bench_$TAG.json
+(cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof/$TAG" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu > "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log" 2>&1) || { echo "rocprof failed"; tail -20 gpurun_out/prof_$TAG.log; exit 1; }
+# the same kernels with one render pipeline: every k_chain launch is a whole frame, the launch the
+# bench line's roofline times (avg_launch_ms) with HIP events
+(cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof/${TAG}_p1" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu --no-bf-roofline --pipes 1 > "$GRAFT_REPO_ROOT/gpurun_out/prof_${TAG}_p1.log" 2>&1) || { echo "rocprof p1 failed"; tail -20 gpurun_out/prof_${TAG}_p1.log; exit 1; }
+bash tools/gpu_workloads.sh $TAG || exit 1
