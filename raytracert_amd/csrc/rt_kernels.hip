@@ -588,6 +588,9 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
 #ifndef RT_WW_SLACK
 #define RT_WW_SLACK 0   // measured: 0 best (4: +5%, 12: +10%, 24: +20% frame time)
 #endif
+#ifndef RT_NODE_BRANCHFREE
+#define RT_NODE_BRANCHFREE 1
+#endif
 #ifndef RT_WW_CURSOR
 #define RT_WW_CURSOR 1   // measured 2% faster C4 and C5 than whole leaves per iteration
 #endif
@@ -631,6 +634,40 @@ __device__ __forceinline__ int32_t node4_next(const Ray4 &R, uint4 a, uint4 b, u
         bool h = te <= tx * 1.00001f;
         if (!kAnyHit) h = h && te <= R.tcull;
         tc[k] = h ? fminf(te, FLT_MAX) : INFINITY;
+    }
+    if (RT_NODE_BRANCHFREE && (!kAnyHit || RT_NODE_BRANCHFREE > 1)) {
+        // Branch-free pushes: the wanted children after the first go to the stack with
+        // unconditional LDS writes when every lane's stack has room (slots past the new top are
+        // scratch); pops the same way. Misses are INFINITY and sort last.
+        const int nh = (tc[0] != INFINITY) + (tc[1] != INFINITY) + (tc[2] != INFINITY) + (tc[3] != INFINITY);
+        if (nh > 1) {
+            cswap(tc[0], rc[0], tc[1], rc[1]);
+            cswap(tc[2], rc[2], tc[3], rc[3]);
+            cswap(tc[0], rc[0], tc[2], rc[2]);
+            cswap(tc[1], rc[1], tc[3], rc[3]);
+            cswap(tc[1], rc[1], tc[2], rc[2]);
+        } else {
+            rc[0] = tc[0] != INFINITY ? rc[0] : tc[1] != INFINITY ? rc[1] : tc[2] != INFINITY ? rc[2] : rc[3];
+        }
+        const int lane = static_cast<int>(threadIdx.x);
+        if (__all(sp + 3 <= stack.cap)) {
+            stack.lds[sp * stack.width + lane] = nh == 4 ? rc[3] : nh == 3 ? rc[2] : rc[1];
+            stack.lds[(sp + 1) * stack.width + lane] = nh == 4 ? rc[2] : rc[1];
+            stack.lds[(sp + 2) * stack.width + lane] = rc[1];
+            sp += max(nh - 1, 0);
+        } else {
+            if (tc[3] != INFINITY) stack.push(sp, rc[3]);
+            if (tc[2] != INFINITY) stack.push(sp, rc[2]);
+            if (tc[1] != INFINITY) stack.push(sp, rc[1]);
+        }
+        if (nh > 0) return rc[0];
+        if (__all(sp <= stack.cap)) {
+            const int32_t top = stack.lds[max(sp - 1, 0) * stack.width + lane];
+            const int32_t r = sp > 0 ? top : kDoneRef;
+            sp = max(sp - 1, 0);
+            return r;
+        }
+        return sp ? stack.pop(sp) : kDoneRef;
     }
     if (!kAnyHit || kSortAnyHit) {
         const int nh = (tc[0] != INFINITY) + (tc[1] != INFINITY) + (tc[2] != INFINITY) + (tc[3] != INFINITY);
