@@ -84,7 +84,7 @@ def parse():
     ap.add_argument("--accel", choices=("bvh", "brute_force"), default="bvh")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c4")
     ap.add_argument("--no-bf-roofline", action="store_true", help="skip the brute-force kernel's roofline frame")
-    ap.add_argument("--pipes", type=int, default=2, help="render pipelines a call's batches overlap on")
+    ap.add_argument("--pipes", type=int, default=1, help="render pipelines a call's batches overlap on")
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
                     help="extra launch-shape knob (Scene.tune), e.g. shadow_virtual=-1; repeatable")
     return ap.parse_args()

@@ -199,10 +199,13 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
 /* ---- tuning (launch-shape knobs; results never depend on them) ------------------------- */
 #define RT_TUNE_XCD_SPLIT 0   /* BVH queue distribution: 0 grid-stride, 1 one static segment per XCD,
                                  2 per-XCD segments with work-stealing wave counters */
-#define RT_TUNE_BVH_GRID  1   /* resident grid (blocks of 128 threads) of the BVH kernels */
+#define RT_TUNE_BVH_GRID  1   /* grid cap (blocks of 128 threads) of the BVH kernels; default 16384: the
+                                 chain launch then gives each wave one 64-sample batch of a C4 frame
+                                 and the dispatcher balances the blocks */
 #define RT_TUNE_BVH_WIDTH 2   /* 4 (default): quantised four-wide nodes; 2: float binary nodes */
 #define RT_TUNE_LDS_STACK 3   /* traversal stack entries per lane kept in LDS; deeper ones in HBM */
-#define RT_TUNE_PIPES     4   /* 1-4 render pipelines (workspace + stream) a call's batches overlap on */
+#define RT_TUNE_PIPES     4   /* 1-4 render pipelines (workspace + stream) a call's batches overlap on
+                                 (default 1) */
 #define RT_TUNE_WAVE_TRAVERSAL 8   /* bit k: closest-hit of chain step k, bit 16+k: its shadow rays,
                                       bit 31: rt_intersect_mesh, walk the four-wide tree once per
                                       wave (coherent rays); default 0: measured no faster on C4,

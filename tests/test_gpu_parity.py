@@ -306,7 +306,8 @@ def test_multi_frame_shard_batch_reassembles(workdir, gpu_available):
                                    {"wave_traversal": -1}, {"wave_traversal": -1, "shadow_virtual": 0},
                                    {"wave_traversal": -1, "lds_stack": 1}, {"chain_from": 0}, {"chain_from": 1},
                                    {"chain_from": 3}, {"chain_from": 255}, {"chain_from": 0, "lds_stack": 1},
-                                   {"chain_from": 1, "bvh_width": 2}, {"chain_from": 0, "pipes": 1}])
+                                   {"chain_from": 1, "bvh_width": 2}, {"chain_from": 0, "pipes": 1},
+                                   {"pipes": 2}, {"pipes": 2, "bvh_grid": 4096}, {"bvh_grid": 65536}])
 def test_launch_shape_knobs_never_change_results(knobs, workdir, gpu_available):
     """Query distribution (grid-stride, static XCD segments, work-stealing XCD queues), tiny grids
     (fewer blocks than XCDs), tree width and the LDS/HBM split of the traversal stack (1 entry in
