@@ -1938,9 +1938,11 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
     const DevScene s = for_width(s0, wide ? 4 : 2);
     auto k = wide ? (s.any_transparent ? k_chain<4, false, false> : k_chain<4, true, false>)
                   : (s.any_transparent ? k_chain<2, false, false> : k_chain<2, true, false>);
+#ifndef RT_WAVE_TIMES   // (the wave-times diagnostic build times the uncounted kernel)
     if (s.work)
         k = wide ? (s.any_transparent ? k_chain<4, false, true> : k_chain<4, true, true>)
                  : (s.any_transparent ? k_chain<2, false, true> : k_chain<2, true, true>);
+#endif
     hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, p, w, first,
                        s.nodes4, s.leaf_recs, s.leaf_idx);
 }

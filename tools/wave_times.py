@@ -28,7 +28,7 @@ sc.reset_stats()
 sc.set_profiling(True, count_work=True)
 sc.render(p)
 sc.set_profiling(False)
-d = sc.diag_read(0, 3 * 8192).reshape(-1, 3).astype(np.int64)
+d = sc.diag_read(0, 3 * 43690).reshape(-1, 3).astype(np.int64)
 d = d[d[:, 1] > 0]
 t0 = d[:, 0].min()
 s, e = (d[:, 0] - t0) * 0.01, (d[:, 1] - t0) * 0.01   # microseconds
