@@ -95,6 +95,9 @@ struct DevWork {
     uint8_t *depth;                 // per sample: number of chain steps
     int32_t *counters;              // [step] main queue sizes (step 0 dense, incl. inactive), [kMaxStepsCounters + step] shadow
     int32_t *wq;                    // [2 * step + shadow] work-queue slots of kWqSlot ints (RT_TUNE_XCD_SPLIT 2)
+    uint32_t *batch_cost;           // chain launch: per 64-sample batch, its wave's duration (100 MHz ticks)
+    int32_t *batch_order;           // chain launch: dispatch order of the batches (cost descending), or unused
+    int32_t *order_scratch;         // counting-sort scratch (kOrderBuckets histogram + offsets)
     int64_t cap;                    // samples per batch
     int32_t steps;                  // chain steps allocated (max_lvl + 1)
 };
@@ -117,8 +120,14 @@ void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int
 void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream);
 // Steps first..max_lvl of every query in Q_first in one launch (closest-hit, shadows, shade per lane).
 void launch_chain(const DevScene &s, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
-                  hipStream_t stream);
+                  hipStream_t stream, bool ordered = false);
 void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t stream);
+// Order the chain launch's 64-sample batches by the durations its last launch measured, longest
+// first (w.batch_cost -> w.batch_order); the next launch over the same batches dispatches in
+// that order (launch_chain(..., ordered = true)).
+constexpr int kOrderBuckets = 128;
+constexpr int kWaveBatch = 64;   // samples per wave batch of the chain launch (one per lane)
+void launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream);
 void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *dst, int32_t n,
                            int32_t *idx, float4 *I, hipStream_t stream);
 

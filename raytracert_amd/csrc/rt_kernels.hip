@@ -1691,10 +1691,14 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
 // current one, which is what the thin last steps spend their time on. The per-ray arithmetic is
 // the per-step kernels' own (the same functions). Query counts per step (ray statistics) are
 // summed per block in LDS and added to the step counters once at the end.
+// Batch order (ordered): wave-sized batch v of the grid-stride walk takes the samples of batch
+// w.batch_order[v]; every wave records its batch's duration in w.batch_cost, from which
+// launch_order_batches prepares the next launch's order (longest first, so the deep reflection
+// chains of a frame start at once instead of trailing it). Placement never changes results.
 template <int W, bool kAnyHit, bool kCount>
 __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CHAIN_WPE))) void k_chain(
     const DevScene sc, const ShadeParams p, DevWork w, int first, const Bvh4Node *__restrict__ n4,
-    const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx) {
+    const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx, int ordered) {
     extern __shared__ int32_t lds_stack[];
     __shared__ int s_q[kChainSteps], s_sh[kChainSteps];
     for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) { s_q[i] = 0; s_sh[i] = 0; }
@@ -1708,7 +1712,11 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
     unsigned long long wt_q = 0;
 #endif
     const int nq = w.counters[first];
-    drive_queries(nq, sc.chain_split & 3, w.wq + (2 * first) * kWqSlot, [&](int j, int end) {
+    drive_queries(nq, sc.chain_split & 3, w.wq + (2 * first) * kWqSlot, [&](int j0, int end) {
+        const int vb = j0 >> 6;   // this wave's batch in dispatch order (wave-uniform when ordered)
+        const int pb = (ordered && (vb << 6) < end) ? w.batch_order[vb] : vb;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        [&](int j) {
         if (j >= end) return;
         if (sc.chain_split & 4) j = nq - 1 - j;   // (diagnostic: reversed order)
         const float4 qo = w.q_org[first & 1][j], qd = w.q_dst[first & 1][j];
@@ -1728,6 +1736,9 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
             dst = sec.dst;
             lvl = sec.lvl;
         }
+        }(ordered ? pb * kWave + (j0 & (kWave - 1)) : j0);
+        if (__lane_id() == 0 && j0 < end)
+            w.batch_cost[pb] = static_cast<uint32_t>(min(__builtin_amdgcn_s_memrealtime() - t0, 0xFFFFFFFFull));
     });
 #ifdef RT_WAVE_TIMES
     for (int off = 32; off > 0; off >>= 1) wt_q += __shfl_xor(wt_q, off);
@@ -1808,6 +1819,56 @@ __global__ __launch_bounds__(kBlock) void k_fold_rays(DevWork w, int32_t n, floa
     if (s >= n) return;
     const V3 c = fold_chain(w, s);
     rgb[3 * s] = c.x; rgb[3 * s + 1] = c.y; rgb[3 * s + 2] = c.z;
+}
+
+// Counting sort of the batches by duration, longest first: bucket = 4 x log2(ticks) plus the two
+// bits below the leading one (quarter-octave buckets); within a bucket the order is arbitrary.
+constexpr int kOrderBlock = 256;
+__device__ __forceinline__ int order_bucket(uint32_t c) {
+    if (c < 4) return kOrderBuckets - 1;
+    const int e = 31 - __clz(c);
+    const int k = 4 * e + static_cast<int>((c >> (e - 2)) & 3u);
+    return kOrderBuckets - 1 - min(k, kOrderBuckets - 1);   // descending duration
+}
+
+__global__ __launch_bounds__(kOrderBlock) void k_order_hist(const uint32_t *__restrict__ cost, int n, int32_t *hist) {
+    __shared__ int h[kOrderBuckets];
+    for (int i = threadIdx.x; i < kOrderBuckets; i += kOrderBlock) h[i] = 0;
+    __syncthreads();
+    for (int i = blockIdx.x * kOrderBlock + threadIdx.x; i < n; i += gridDim.x * kOrderBlock) atomicAdd(&h[order_bucket(cost[i])], 1);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kOrderBuckets; i += kOrderBlock)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+__global__ __launch_bounds__(kOrderBuckets) void k_order_scan(int32_t *hist) {
+    __shared__ int h[kOrderBuckets];
+    h[threadIdx.x] = hist[threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int i = 0; i < kOrderBuckets; ++i) { const int c = h[i]; h[i] = acc; acc += c; }
+    }
+    __syncthreads();
+    hist[threadIdx.x] = h[threadIdx.x];   // bucket offsets; the scatter advances them
+}
+
+__global__ __launch_bounds__(kOrderBlock) void k_order_scatter(const uint32_t *__restrict__ cost, int n, int32_t *offs,
+                                                            int32_t *__restrict__ order) {
+    __shared__ int h[kOrderBuckets], base[kOrderBuckets];
+    for (int i0 = blockIdx.x * kOrderBlock; i0 < n; i0 += gridDim.x * kOrderBlock) {   // block-uniform
+        for (int i = threadIdx.x; i < kOrderBuckets; i += kOrderBlock) h[i] = 0;
+        __syncthreads();
+        const int i = i0 + static_cast<int>(threadIdx.x);
+        int b = 0, r = 0;
+        if (i < n) { b = order_bucket(cost[i]); r = atomicAdd(&h[b], 1); }
+        __syncthreads();
+        for (int k = threadIdx.x; k < kOrderBuckets; k += kOrderBlock)
+            if (h[k]) base[k] = atomicAdd(&offs[k], h[k]);
+        __syncthreads();
+        if (i < n) order[base[b] + r] = i;
+        __syncthreads();
+    }
 }
 
 inline unsigned grid_for(int64_t n) { return static_cast<unsigned>((n + kBlock - 1) / kBlock); }
@@ -1932,7 +1993,7 @@ void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int
 }
 
 void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
-                  hipStream_t stream) {
+                  hipStream_t stream, bool ordered) {
     if (capacity <= 0) return;
     const bool wide = tree_variant(s0, -1) == 4;
     const DevScene s = for_width(s0, wide ? 4 : 2);
@@ -1944,7 +2005,18 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
                  : (s.any_transparent ? k_chain<2, false, true> : k_chain<2, true, true>);
 #endif
     hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, p, w, first,
-                       s.nodes4, s.leaf_recs, s.leaf_idx);
+                       s.nodes4, s.leaf_recs, s.leaf_idx, ordered ? 1 : 0);
+}
+
+void launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream) {
+    if (nbatches <= 0) return;
+    const int n = static_cast<int>(nbatches);
+    hipMemsetAsync(w.order_scratch, 0, sizeof(int32_t) * kOrderBuckets, stream);
+    const unsigned grid = static_cast<unsigned>(std::min<int64_t>((nbatches + kOrderBlock - 1) / kOrderBlock, 1024));
+    hipLaunchKernelGGL(k_order_hist, dim3(grid), dim3(kOrderBlock), 0, stream, w.batch_cost, n, w.order_scratch);
+    hipLaunchKernelGGL(k_order_scan, dim3(1), dim3(kOrderBuckets), 0, stream, w.order_scratch);
+    hipLaunchKernelGGL(k_order_scatter, dim3(grid), dim3(kOrderBlock), 0, stream, w.batch_cost, n, w.order_scratch,
+                       w.batch_order);
 }
 
 void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream) {

@@ -271,6 +271,22 @@ def test_c4_full_frame_bvh_equals_brute_force(workdir, gpu_available):
         assert np.array_equal(xf.view(np.uint32), bf.view(np.uint32))
 
 
+def test_batch_order_from_previous_launch_keeps_results(workdir, gpu_available):
+    """RT_TUNE_BATCH_ORDER: the first render dispatches the chain's batches in screen order and
+    times them; the next renders over the same batches dispatch them longest first. Every render
+    is byte-identical with identical ray counts, with the order on or off."""
+    p = R.RenderParams(width=320, height=180, pf=1, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
+    with R.Scene.load(scene_path("syn:C4", workdir), device=0) as sc:
+        sc.tune("batch_order", 0)
+        ref, fref, cref = sc.render(p, want_f32=True)
+        sc.tune("batch_order", 1)
+        for _ in range(3):
+            u8, f32, counts = sc.render(p, want_f32=True)
+            assert [int(c) for c in counts] == [int(c) for c in cref]
+            assert np.array_equal(u8, ref)
+            assert np.array_equal(f32.view(np.uint32), fref.view(np.uint32))
+
+
 def test_multi_frame_shard_batch_reassembles(workdir, gpu_available):
     """Weak-scaling step shape: a batch of 3 frames of one view, ids g = f*T + t interleaved over 3
     ranks, one rt_render_tiles_device call per rank; every assembled frame equals the render."""

@@ -60,3 +60,20 @@ for v in groups.values():
         ends_by_rank.setdefault(r, []).append(e[i])
 print(json.dumps({"simds": len(groups), "waves_per_simd_pcts": [int(np.percentile(sizes, q)) for q in (5, 50, 95)],
                   "mean_end_us_by_start_rank_on_simd": {r: round(float(np.mean(x)), 1) for r, x in sorted(ends_by_rank.items()) if len(x) > 50}}))
+# where the long waves are: wave w takes samples [64 w, 64 w + 64) of the tile-major queue
+# (one batch per wave when the grid covers the frame); map them to 16x16 tiles on the screen
+if len(d) * 64 >= p.width * p.height:
+    tiles_x = (p.width + 15) // 16
+    order = np.argsort(-life)
+    top = [(int(i) * 64 // 256 % tiles_x, int(i) * 64 // 256 // tiles_x, round(float(life[i]), 1)) for i in order[:20]]
+    print(json.dumps({"slowest_waves_tile_xy_us": top}))
+    tiles_y = (p.height + 15) // 16
+    grid = np.zeros((tiles_y, tiles_x))
+    for i in range(len(d)):
+        t = i * 64 // 256
+        if t < tiles_x * tiles_y:
+            grid[t // tiles_x, t % tiles_x] = max(grid[t // tiles_x, t % tiles_x], life[i])
+    coarse = grid[: tiles_y // 6 * 6, : tiles_x // 10 * 10].reshape(tiles_y // 6, 6, tiles_x // 10, 10).max(axis=(1, 3))
+    print("max wave life (us) per 160x96-pixel block:")
+    for row in coarse:
+        print(" ".join(f"{v:5.0f}" for v in row))
