@@ -161,9 +161,17 @@ def main():
             work.wait()
         return rdist.assemble_plan_torch(gathered, plan, index) if rank == 0 else None
 
+    single = world == 1 and plan.frames == 1
+    if single:   # one GPU: the library writes the row-major frame itself (no gather, no un-permute)
+        fbufs = [torch.zeros(HEIGHT * WIDTH * 3, dtype=torch.uint8, device=dev) for _ in range(2)]
+
     def step(i):
         """Render step i's shard, start its gather (async, on the collective's stream) and finish
         step i-1's: the gather of one step overlaps the next step's render."""
+        if single:
+            fb = fbufs[i % 2]
+            scene.render_frame_device(cparams, TILE, TILE, fb.data_ptr(), fb.numel(), stream.cuda_stream)
+            return fb.view(1, HEIGHT, WIDTH, 3)
         render_shard(buf=bufs[i % 2])
         pending.append(rdist.gather_shards(bufs[i % 2], rank, world, async_op=True))
         return finish(pending.pop(0)) if len(pending) > 1 else None

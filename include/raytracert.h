@@ -17,6 +17,7 @@
  *   rt_render_tile        the 'r'-key frame loop            main.cpp:340-411 (loop :355-395,
  *                         + RGBValue clamp :24-42 + Image::writeImage quantisation :102-128)
  *   rt_render_tiles_device  same loop, interleaved tile shard into a device buffer (multi-GPU)
+ *   rt_render_frame_device  same loop, the whole frame into a device buffer (single GPU)
  *   rt_default_corners    produceRay for the 4 corners      main.cpp:300-325,355-358 (+ reshape :288-296)
  *   rt_write_ppm          Image::writeImage                 main.cpp:102-128
  *
@@ -163,6 +164,11 @@ int rt_render_tile(rt_scene *scene, const rt_params *params, int32_t x0, int32_t
  * later work queued on it sees the finished tiles (the renderer forks its pipelines from it and
  * joins them back). The call returns after enqueueing (no host synchronisation) unless
  * counts != NULL. Returns the number of tiles written via n_tiles_out. */
+/* The whole frame, row-major (height x width x 3 bytes, the PPM's pixel order), into the DEVICE
+ * buffer d_out_u8, rendered in tile_w x tile_h tiles; stream semantics as rt_render_tiles_device.
+ * The single-GPU form of the shard + gather path (no un-permute needed). */
+int rt_render_frame_device(rt_scene *scene, const rt_params *params, int32_t tile_w, int32_t tile_h, void *d_out_u8,
+                           size_t out_capacity, void *stream, uint64_t counts[3]);
 int rt_render_tiles_device(rt_scene *scene, const rt_params *params, int32_t tile_w, int32_t tile_h,
                            int32_t frames, int32_t first, int32_t stride, void *d_out_u8, size_t out_capacity,
                            void *stream, int32_t *n_tiles_out, uint64_t counts[3]);

@@ -90,6 +90,7 @@ _SIGNATURES = {
     "rt_trace_rays": ([_VP, C.POINTER(RtParams), _VP, _VP, C.c_int32, _VP, _VP], C.c_int),
     "rt_debug_trace": ([_VP, C.POINTER(RtParams), _VP, _VP, _VP, C.c_int32, C.POINTER(C.c_int32), _VP], C.c_int),
     "rt_render_tile": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP, _VP, _VP], C.c_int),
+    "rt_render_frame_device": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, _VP, C.c_size_t, _VP, _VP], C.c_int),
     "rt_render_tiles_device": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP,
                                 C.c_size_t, _VP, C.POINTER(C.c_int32), _VP], C.c_int),
     "rt_default_corners": ([C.c_int32, C.c_int32, _VP], C.c_int),

@@ -218,6 +218,15 @@ class Scene:
                                            C.byref(n_tiles), _ptr(counts)))
         return n_tiles.value, counts
 
+    def render_frame_device(self, params: RenderParams | RtParams, tile_w: int, tile_h: int, out_ptr: int,
+                            out_capacity: int, stream_ptr: int | None = None, want_counts: bool = False):
+        """The whole frame, row-major H x W x 3 bytes, into a device buffer (rt_render_frame_device)."""
+        p = params.to_c() if isinstance(params, RenderParams) else params
+        counts = np.zeros(3, np.uint64) if want_counts else None
+        check(lib().rt_render_frame_device(self._h, C.byref(p), tile_w, tile_h, C.c_void_p(out_ptr), out_capacity,
+                                           C.c_void_p(stream_ptr) if stream_ptr else None, _ptr(counts)))
+        return counts
+
     # -- acceleration ------------------------------------------------------------------------
     def set_accel(self, mode) -> None:
         """'bvh' / 'brute_force' (or RT_ACCEL_* ints). Results are identical either way."""

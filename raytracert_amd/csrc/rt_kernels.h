@@ -110,6 +110,7 @@ constexpr int kWqStride = 16;                // one 64-B line per segment counte
 constexpr int kWqSlot = 8 * kWqStride;       // eight segments (one per XCD) per launch
 
 // Launchers (all asynchronous on `stream`).
+// k_gen_primary also zeroes w.counters (then counter 0 = the batch's samples) and w.wq.
 void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream);
 void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevWork &w, hipStream_t stream);
 void launch_closest_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream);
@@ -122,9 +123,9 @@ void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *
 void launch_chain(const DevScene &s, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
                   hipStream_t stream, bool ordered = false);
 void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t stream);
-// Order the chain launch's 64-sample batches by the durations its last launch measured, longest
-// first (w.batch_cost -> w.batch_order); the next launch over the same batches dispatches in
-// that order (launch_chain(..., ordered = true)).
+// Batch order: the chain launch's 64-sample batches sorted by the durations it measured, longest
+// first (w.batch_cost -> w.batch_order); the next launch over the same batches dispatches in that
+// order (launch_chain(..., ordered = true)). A counting sort: one fill and three small launches.
 constexpr int kOrderBuckets = 128;
 constexpr int kWaveBatch = 64;   // samples per wave batch of the chain launch (one per lane)
 void launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream);

@@ -1380,12 +1380,15 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
     return h;
 }
 
+// Also resets the batch's queue counters and work-queue slots (counter 0 = the queue's size), so
+// no separate fills precede the batch.
 __global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWork w) {
     const int spp = g.pfx * g.pfy;
     const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th * spp;
     const int64_t s = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (s < 2 * kMaxStepsCounters) w.counters[s] = s == 0 ? static_cast<int32_t>(n) : 0;
+    if (s < 2 * static_cast<int64_t>(w.steps) * kWqSlot) w.wq[s] = 0;
     if (s >= n) return;
-    if (s == 0) w.counters[0] = static_cast<int32_t>(n);
     const int64_t pix = s / spp;
     const int sub = static_cast<int>(s - pix * spp);
     const int subx = sub / g.pfy, suby = sub - subx * g.pfy;   // subx outer, suby inner (:377-378)
@@ -1878,7 +1881,8 @@ inline unsigned grid_for(int64_t n) { return static_cast<unsigned>((n + kBlock -
 void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream) {
     const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th * g.pfx * g.pfy;
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_gen_primary, dim3(grid_for(n)), dim3(kBlock), 0, stream, g, w);
+    const int64_t clear = std::max<int64_t>(2 * kMaxStepsCounters, 2 * static_cast<int64_t>(w.steps) * kWqSlot);
+    hipLaunchKernelGGL(k_gen_primary, dim3(grid_for(std::max(n, clear))), dim3(kBlock), 0, stream, g, w);
 }
 
 void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevWork &w, hipStream_t stream) {
@@ -2008,6 +2012,12 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
                        s.nodes4, s.leaf_recs, s.leaf_idx, ordered ? 1 : 0);
 }
 
+void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream) {
+    const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th;
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_frame, dim3(grid_for(n)), dim3(kBlock), 0, stream, g, w, out_u8, out_f32);
+}
+
 void launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream) {
     if (nbatches <= 0) return;
     const int n = static_cast<int>(nbatches);
@@ -2017,12 +2027,6 @@ void launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream
     hipLaunchKernelGGL(k_order_scan, dim3(1), dim3(kOrderBuckets), 0, stream, w.order_scratch);
     hipLaunchKernelGGL(k_order_scatter, dim3(grid), dim3(kOrderBlock), 0, stream, w.batch_cost, n, w.order_scratch,
                        w.batch_order);
-}
-
-void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream) {
-    const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th;
-    if (n <= 0) return;
-    hipLaunchKernelGGL(k_frame, dim3(grid_for(n)), dim3(kBlock), 0, stream, g, w, out_u8, out_f32);
 }
 
 void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t stream) {

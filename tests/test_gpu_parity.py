@@ -147,6 +147,23 @@ def test_sharded_tiles_reassemble_to_full_frame(workdir, gpu_available):
     assert [int(x) for x in total] == [int(x) for x in counts]
 
 
+@pytest.mark.parametrize("size,pf", [((100, 70), 2), ((1920, 1080), 1)])
+def test_frame_device_equals_rectangle_render(size, pf, workdir, gpu_available):
+    """rt_render_frame_device (the single-GPU bench path) writes the row-major frame the rectangle
+    render returns, with the same ray counts, twice in a row (the second launch batch-ordered)."""
+    import torch
+    w, h = size
+    p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
+    with R.Scene.load(scene_path("syn:C4" if w > 1000 else "syn:F3", workdir), device=0) as sc:
+        full, _, counts = sc.render(p)
+        buf = torch.full((h * w * 3,), 7, dtype=torch.uint8, device="cuda:0")
+        for _ in range(2):
+            c = sc.render_frame_device(p, 16, 16, buf.data_ptr(), buf.numel(), torch.cuda.current_stream().cuda_stream,
+                                       want_counts=True)
+            assert np.array_equal(buf.view(h, w, 3).cpu().numpy(), full)
+            assert [int(x) for x in c] == [int(x) for x in counts]
+
+
 def test_transparent_shadow_path_and_deep_chain(workdir, gpu_available):
     """F4 scenes exercise the closest-hit shadow path (a transparent material exists) and
     chains deeper than 2; the golden comparison above covers bytes, this checks counts against
