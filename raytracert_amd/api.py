@@ -254,7 +254,8 @@ class Scene:
              "pipe_batches": _capi.TUNE_PIPE_BATCHES, "pipe_priority": _capi.TUNE_PIPE_PRIORITY,
              "wave_traversal": _capi.TUNE_WAVE_TRAVERSAL, "chain_from": _capi.TUNE_CHAIN_FROM,
              "chain_split": _capi.TUNE_CHAIN_SPLIT, "top_nodes": _capi.TUNE_TOP_NODES,
-             "batch_order": _capi.TUNE_BATCH_ORDER}[knob]
+             "batch_order": _capi.TUNE_BATCH_ORDER,
+             "order_every": _capi.TUNE_ORDER_EVERY}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
 
     def bvh_digest(self) -> int:

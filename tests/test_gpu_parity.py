@@ -297,7 +297,8 @@ def test_batch_order_from_previous_launch_keeps_results(workdir, gpu_available):
         sc.tune("batch_order", 0)
         ref, fref, cref = sc.render(p, want_f32=True)
         sc.tune("batch_order", 1)
-        for _ in range(3):
+        sc.tune("order_every", 2)
+        for _ in range(5):
             u8, f32, counts = sc.render(p, want_f32=True)
             assert [int(c) for c in counts] == [int(c) for c in cref]
             assert np.array_equal(u8, ref)
