@@ -224,6 +224,8 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
                                     same batches measured (the first launch runs in screen order) */
 #define RT_TUNE_ORDER_EVERY 17  /* batch order re-sorted every this many launches over the same batches
                                     (default 8; 1: every launch); the durations are measured every time */
+#define RT_TUNE_FUSE_PIXELS 18  /* 1 (default): with one sample per pixel the chain launch writes each
+                                    pixel when its chain ends (no separate frame pass); 0: frame pass */
 #define RT_TUNE_TOP_NODES 13     /* four-wide nodes of the tree's top levels (breadth-first, the first
                                     ones in the node array) each block reads from an LDS copy (0-85) */
 #define RT_TUNE_CHAIN_SPLIT 12   /* query distribution of the chain launch: as RT_TUNE_XCD_SPLIT, or 3: 64-query

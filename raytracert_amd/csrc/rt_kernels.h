@@ -95,6 +95,7 @@ struct DevWork {
     uint8_t *depth;                 // per sample: number of chain steps
     int32_t *counters;              // [step] main queue sizes (step 0 dense, incl. inactive), [kMaxStepsCounters + step] shadow
     int32_t *wq;                    // [2 * step + shadow] work-queue slots of kWqSlot ints (RT_TUNE_XCD_SPLIT 2)
+    int32_t *pix_out;               // per sample (fused pixel writes, one sample per pixel): its pixel's output index
     uint32_t *batch_cost;           // chain launch: per 64-sample batch, its wave's duration (100 MHz ticks)
     int32_t *batch_order;           // chain launch: dispatch order of the batches (cost descending), or unused
     int32_t *order_scratch;         // counting-sort scratch (kOrderBuckets histogram + offsets)
@@ -110,8 +111,11 @@ constexpr int kWqStride = 16;                // one 64-B line per segment counte
 constexpr int kWqSlot = 8 * kWqStride;       // eight segments (one per XCD) per launch
 
 // Launchers (all asynchronous on `stream`).
-// k_gen_primary also zeroes w.counters (then counter 0 = the batch's samples) and w.wq.
-void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream);
+// k_gen_primary also zeroes w.counters (then counter 0 = the batch's samples) and w.wq. fused (one
+// sample per pixel): the chain launch will write the pixels; records w.pix_out and writes the
+// pixels outside the frame.
+void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream, bool fused = false,
+                        uint8_t *out_u8 = nullptr);
 void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevWork &w, hipStream_t stream);
 void launch_closest_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream);
 void launch_shadow_gen(const DevScene &s, const DevWork &w, const ShadeParams &p, int64_t capacity, hipStream_t stream);
@@ -120,8 +124,10 @@ void launch_shadow_hit(const DevScene &s, const DevWork &w, const ShadeParams &p
 void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int64_t capacity, hipStream_t stream);
 void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream);
 // Steps first..max_lvl of every query in Q_first in one launch (closest-hit, shadows, shade per lane).
+// out_u8/out_f32 (first == 0, after launch_gen_primary(fused)): each sample's pixel is written at
+// the end of its chain with k_frame's arithmetic, so no k_frame follows.
 void launch_chain(const DevScene &s, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
-                  hipStream_t stream, bool ordered = false);
+                  hipStream_t stream, bool ordered = false, uint8_t *out_u8 = nullptr, float *out_f32 = nullptr);
 void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t stream);
 // Batch order: the chain launch's 64-sample batches sorted by the durations it measured, longest
 // first (w.batch_cost -> w.batch_order); the next launch over the same batches dispatches in that

@@ -1381,8 +1381,11 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
 }
 
 // Also resets the batch's queue counters and work-queue slots (counter 0 = the queue's size), so
-// no separate fills precede the batch.
-__global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWork w) {
+// no separate fills precede the batch. fused (one sample per pixel; the chain launch writes the
+// pixels): also records each sample's pixel index in w.pix_out and writes the pixels outside the
+// frame black in the tile-major layout, as k_frame does.
+__global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWork w, uint8_t *__restrict__ fused_u8,
+                                                        int fused) {
     const int spp = g.pfx * g.pfy;
     const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th * spp;
     const int64_t s = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
@@ -1394,6 +1397,12 @@ __global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWo
     const int subx = sub / g.pfy, suby = sub - subx * g.pfy;   // subx outer, suby inner (:377-378)
     int x, y;
     const bool valid = decode_pixel(g, pix, x, y);
+    if (fused) {   // (spp == 1: s == pix)
+        const int64_t px = g.out_mode == 0 ? static_cast<int64_t>(g.tile0) * g.tw * g.th + pix
+                                           : static_cast<int64_t>(y - g.oy) * g.cw + (x - g.ox);
+        if (valid) w.pix_out[s] = static_cast<int32_t>(px);
+        else if (g.out_mode == 0 && fused_u8) { fused_u8[3 * px] = 0; fused_u8[3 * px + 1] = 0; fused_u8[3 * px + 2] = 0; }
+    }
     V3 origin = mk(0, 0, 0), dest = mk(0, 0, 0);
     if (valid) {
         float fx = static_cast<float>(subx), fy = static_cast<float>(suby);
@@ -1637,6 +1646,43 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(const DevScene sc, const 
     }
 }
 
+// Fold one sample's chain back to front: c_k = local_k + coef_k * c_{k+1} (the order in which
+// shade() adds the value returned by the recursive trace(), raytracing.cpp:359,363).
+__device__ __forceinline__ V3 fold_chain(const DevWork &w, int64_t s) {
+    V3 c = mk(0, 0, 0);
+    const int d = w.depth[s];
+    for (int k = d - 1; k >= 0; --k) {
+        const int64_t ci = static_cast<int64_t>(k) * w.cap + s;
+        const float4 L = w.chain_local[ci];
+        const uint32_t st = static_cast<uint32_t>(as_int(L.w));
+        if (st == kChildTrace) {
+            const float4 K = w.chain_coef[ci];
+            c = add(mk(L.x, L.y, L.z), mul(mk(K.x, K.y, K.z), c));
+        } else if (st == kChildZero) {
+            c = add(mk(L.x, L.y, L.z), mk(0.0f, 0.0f, 0.0f));
+        } else {
+            c = mk(L.x, L.y, L.z);
+        }
+    }
+    return c;
+}
+
+// RGBValue clamp (main.cpp:29-41) and the (unsigned char)(v*255) quantisation (main.cpp:117;
+// NaN -> 0) of one pixel's averaged colour, at element offset o.
+__device__ __forceinline__ void store_pixel(V3 rgb, int64_t o, uint8_t *__restrict__ out_u8, float *__restrict__ out_f32) {
+    float c[3] = {rgb.x, rgb.y, rgb.z};
+    for (int k = 0; k < 3; ++k) {
+        float v = c[k];
+        if (v > 1) v = 1.0f;
+        if (v < 0) v = 0.0f;
+        if (out_f32) out_f32[o + k] = v;
+        if (out_u8) {
+            const float q = v * 255.0f;
+            out_u8[o + k] = (q == q) ? static_cast<uint8_t>(static_cast<int>(q)) : 0;
+        }
+    }
+}
+
 constexpr int kChainSteps = 256;   // max_lvl <= 254
 #ifndef RT_CHAIN_WPE
 #define RT_CHAIN_WPE 6   // measured: 6 (80 VGPRs, 36 B spill) beats 5 (92, none) and 7
@@ -1701,7 +1747,8 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
 template <int W, bool kAnyHit, bool kCount>
 __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CHAIN_WPE))) void k_chain(
     const DevScene sc, const ShadeParams p, DevWork w, int first, const Bvh4Node *__restrict__ n4,
-    const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx, int ordered) {
+    const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx, int ordered, uint8_t *__restrict__ out_u8,
+    float *__restrict__ out_f32) {
     extern __shared__ int32_t lds_stack[];
     __shared__ int s_q[kChainSteps], s_sh[kChainSteps];
     for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) { s_q[i] = 0; s_sh[i] = 0; }
@@ -1739,6 +1786,11 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
             dst = sec.dst;
             lvl = sec.lvl;
         }
+        if (out_u8 || out_f32) {   // fused pixel (one sample per pixel): k_frame's fold, /1, clamp, quantise
+            V3 rgb = fold_chain(w, sample);
+            rgb = mk(rgb.x / 1.0f, rgb.y / 1.0f, rgb.z / 1.0f);   // operator/ by float(pf^2), Vec3D.h:36-38
+            store_pixel(rgb, 3 * static_cast<int64_t>(w.pix_out[sample]), out_u8, out_f32);
+        }
         }(ordered ? pb * kWave + (j0 & (kWave - 1)) : j0);
         if (__lane_id() == 0 && j0 < end)
             w.batch_cost[pb] = static_cast<uint32_t>(min(__builtin_amdgcn_s_memrealtime() - t0, 0xFFFFFFFFull));
@@ -1762,27 +1814,6 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
     }
 }
 
-// Fold one sample's chain back to front: c_k = local_k + coef_k * c_{k+1} (the order in which
-// shade() adds the value returned by the recursive trace(), raytracing.cpp:359,363).
-__device__ __forceinline__ V3 fold_chain(const DevWork &w, int64_t s) {
-    V3 c = mk(0, 0, 0);
-    const int d = w.depth[s];
-    for (int k = d - 1; k >= 0; --k) {
-        const int64_t ci = static_cast<int64_t>(k) * w.cap + s;
-        const float4 L = w.chain_local[ci];
-        const uint32_t st = static_cast<uint32_t>(as_int(L.w));
-        if (st == kChildTrace) {
-            const float4 K = w.chain_coef[ci];
-            c = add(mk(L.x, L.y, L.z), mul(mk(K.x, K.y, K.z), c));
-        } else if (st == kChildZero) {
-            c = add(mk(L.x, L.y, L.z), mk(0.0f, 0.0f, 0.0f));
-        } else {
-            c = mk(L.x, L.y, L.z);
-        }
-    }
-    return c;
-}
-
 // Frame: per pixel, sum sub-samples (subx outer, suby inner), divide by pf^2 (main.cpp:391),
 // clamp (RGBValue, main.cpp:29-41), quantise with truncation (main.cpp:117; NaN -> 0).
 __global__ __launch_bounds__(kBlock) void k_frame(const FrameGeom g, DevWork w, uint8_t *__restrict__ out_u8,
@@ -1804,17 +1835,7 @@ __global__ __launch_bounds__(kBlock) void k_frame(const FrameGeom g, DevWork w, 
     for (int sub = 0; sub < spp; ++sub) rgb = add(rgb, fold_chain(w, pix * spp + sub));
     const float div = static_cast<float>(spp);
     rgb = mk(rgb.x / div, rgb.y / div, rgb.z / div);                 // operator/, Vec3D.h:36-38
-    float c[3] = {rgb.x, rgb.y, rgb.z};
-    for (int k = 0; k < 3; ++k) {
-        float v = c[k];
-        if (v > 1) v = 1.0f;
-        if (v < 0) v = 0.0f;
-        if (out_f32) out_f32[o + k] = v;
-        if (out_u8) {
-            const float q = v * 255.0f;
-            out_u8[o + k] = (q == q) ? static_cast<uint8_t>(static_cast<int>(q)) : 0;
-        }
-    }
+    store_pixel(rgb, o, out_u8, out_f32);
 }
 
 __global__ __launch_bounds__(kBlock) void k_fold_rays(DevWork w, int32_t n, float *__restrict__ rgb) {
@@ -1878,11 +1899,12 @@ inline unsigned grid_for(int64_t n) { return static_cast<unsigned>((n + kBlock -
 
 }  // namespace
 
-void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream) {
+void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream, bool fused, uint8_t *out_u8) {
     const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th * g.pfx * g.pfy;
     if (n <= 0) return;
     const int64_t clear = std::max<int64_t>(2 * kMaxStepsCounters, 2 * static_cast<int64_t>(w.steps) * kWqSlot);
-    hipLaunchKernelGGL(k_gen_primary, dim3(grid_for(std::max(n, clear))), dim3(kBlock), 0, stream, g, w);
+    hipLaunchKernelGGL(k_gen_primary, dim3(grid_for(std::max(n, clear))), dim3(kBlock), 0, stream, g, w, out_u8,
+                       fused ? 1 : 0);
 }
 
 void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevWork &w, hipStream_t stream) {
@@ -1997,7 +2019,7 @@ void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int
 }
 
 void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
-                  hipStream_t stream, bool ordered) {
+                  hipStream_t stream, bool ordered, uint8_t *out_u8, float *out_f32) {
     if (capacity <= 0) return;
     const bool wide = tree_variant(s0, -1) == 4;
     const DevScene s = for_width(s0, wide ? 4 : 2);
@@ -2009,7 +2031,7 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
                  : (s.any_transparent ? k_chain<2, false, true> : k_chain<2, true, true>);
 #endif
     hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, p, w, first,
-                       s.nodes4, s.leaf_recs, s.leaf_idx, ordered ? 1 : 0);
+                       s.nodes4, s.leaf_recs, s.leaf_idx, ordered ? 1 : 0, out_u8, out_f32);
 }
 
 void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream) {

@@ -164,6 +164,37 @@ def test_frame_device_equals_rectangle_render(size, pf, workdir, gpu_available):
             assert [int(x) for x in c] == [int(x) for x in counts]
 
 
+@pytest.mark.parametrize("spec,size,want_f32", [("syn:F3", (100, 70), True), ("syn:C4", (1920, 1080), False),
+                                                 ("syn:F4", (37, 23), True)])
+def test_fused_pixel_writes_equal_frame_pass(spec, size, want_f32, workdir, gpu_available):
+    """RT_TUNE_FUSE_PIXELS: with one sample per pixel the chain launch writes each pixel when its
+    chain ends. Bytes, floats and ray counts equal the separate frame pass's, for the rectangle
+    render, the whole-frame device render and the tile-major shard layout (whose pixels outside
+    the frame are written black: ragged sizes leave partial tiles)."""
+    import torch
+    w, h = size
+    p = R.RenderParams(width=w, height=h, pf=1, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
+    ntiles = ((w + 15) // 16) * ((h + 15) // 16)
+    out = {}
+    with R.Scene.load(scene_path(spec, workdir), device=0) as sc:
+        for fuse in (0, 1):
+            sc.tune("fuse_pixels", fuse)
+            u8, f32, c = sc.render(p, want_f32=want_f32)
+            fb = torch.full((h * w * 3,), 7, dtype=torch.uint8, device="cuda:0")
+            sc.render_frame_device(p, 16, 16, fb.data_ptr(), fb.numel(), torch.cuda.current_stream().cuda_stream)
+            tb = torch.full((ntiles * 256 * 3,), 7, dtype=torch.uint8, device="cuda:0")
+            n, tc = sc.render_tiles_device(p, 16, 16, 0, 1, tb.data_ptr(), tb.numel(),
+                                           torch.cuda.current_stream().cuda_stream, want_counts=True)
+            assert n == ntiles
+            out[fuse] = (u8, f32, [int(x) for x in c], fb.cpu().numpy(), tb.cpu().numpy(), [int(x) for x in tc])
+    a, b = out[0], out[1]
+    assert np.array_equal(a[0], b[0]) and a[2] == b[2] and a[5] == b[5]
+    if want_f32:
+        assert np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32))
+    assert np.array_equal(a[3], b[3]) and np.array_equal(b[3].reshape(h, w, 3), b[0])
+    assert np.array_equal(a[4], b[4])
+
+
 def test_transparent_shadow_path_and_deep_chain(workdir, gpu_available):
     """F4 scenes exercise the closest-hit shadow path (a transparent material exists) and
     chains deeper than 2; the golden comparison above covers bytes, this checks counts against
@@ -341,7 +372,8 @@ def test_multi_frame_shard_batch_reassembles(workdir, gpu_available):
                                    {"wave_traversal": -1, "lds_stack": 1}, {"chain_from": 0}, {"chain_from": 1},
                                    {"chain_from": 3}, {"chain_from": 255}, {"chain_from": 0, "lds_stack": 1},
                                    {"chain_from": 1, "bvh_width": 2}, {"chain_from": 0, "pipes": 1},
-                                   {"pipes": 2}, {"pipes": 2, "bvh_grid": 4096}, {"bvh_grid": 65536}])
+                                   {"pipes": 2}, {"pipes": 2, "bvh_grid": 4096}, {"bvh_grid": 65536},
+                                   {"fuse_pixels": 0}])
 def test_launch_shape_knobs_never_change_results(knobs, workdir, gpu_available):
     """Query distribution (grid-stride, static XCD segments, work-stealing XCD queues), tiny grids
     (fewer blocks than XCDs), tree width and the LDS/HBM split of the traversal stack (1 entry in
