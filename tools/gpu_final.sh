@@ -15,7 +15,6 @@ python3 tools/pmc_summary.py gpurun_out/pmc/$TAG gpurun_out/${TAG}_pmc.json > /d
 timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "bench failed"; tail -30 gpurun_out/bench_$TAG.err; exit 1; }
 cat gpurun_out/bench_$TAG.json
 (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof/$TAG" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu > "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log" 2>&1) || { echo "rocprof failed"; tail -20 gpurun_out/prof_$TAG.log; exit 1; }
-# the same kernels with one render pipeline: every k_chain launch is a whole frame, the launch the
-# bench line's roofline times (avg_launch_ms) with HIP events
-(cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof/${TAG}_p1" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu --no-bf-roofline --pipes 1 > "$GRAFT_REPO_ROOT/gpurun_out/prof_${TAG}_p1.log" 2>&1) || { echo "rocprof p1 failed"; tail -20 gpurun_out/prof_${TAG}_p1.log; exit 1; }
+# the same kernels with two render pipelines (the frame split in batches that overlap)
+(cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof/${TAG}_p2" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu --no-bf-roofline --pipes 2 > "$GRAFT_REPO_ROOT/gpurun_out/prof_${TAG}_p2.log" 2>&1) || { echo "rocprof p2 failed"; tail -20 gpurun_out/prof_${TAG}_p2.log; exit 1; }
 bash tools/gpu_workloads.sh $TAG || exit 1
