@@ -221,11 +221,13 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
                                     >= max_lvl + 1: every step its own launches) */
 #define RT_TUNE_BATCH_ORDER 15  /* 1 (default): the chain launch dispatches its 64-sample batches longest
                                     first, by the durations the pipeline's previous launch over the
-                                    same batches measured (the first launch runs in screen order) */
+                                    same batches measured (the first launch runs in screen order);
+                                    2: the same within eight screen bands, one per XCD (L2 locality) */
 #define RT_TUNE_ORDER_EVERY 17  /* batch order re-sorted every this many launches over the same batches
                                     (default 8; 1: every launch); the durations are measured every time */
-#define RT_TUNE_FUSE_PIXELS 18  /* 1 (default): with one sample per pixel the chain launch writes each
-                                    pixel when its chain ends (no separate frame pass); 0: frame pass */
+#define RT_TUNE_FUSE_PIXELS 18  /* 1 (default): the chain launch writes each pixel when its samples'
+                                    chains end (no separate frame pass) when pf*pf divides 64;
+                                    0: always the frame pass */
 #define RT_TUNE_TOP_NODES 13     /* four-wide nodes of the tree's top levels (breadth-first, the first
                                     ones in the node array) each block reads from an LDS copy (0-85) */
 #define RT_TUNE_CHAIN_SPLIT 12   /* query distribution of the chain launch: as RT_TUNE_XCD_SPLIT, or 3: 64-query

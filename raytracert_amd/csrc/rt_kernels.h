@@ -95,10 +95,10 @@ struct DevWork {
     uint8_t *depth;                 // per sample: number of chain steps
     int32_t *counters;              // [step] main queue sizes (step 0 dense, incl. inactive), [kMaxStepsCounters + step] shadow
     int32_t *wq;                    // [2 * step + shadow] work-queue slots of kWqSlot ints (RT_TUNE_XCD_SPLIT 2)
-    int32_t *pix_out;               // per sample (fused pixel writes, one sample per pixel): its pixel's output index
+    int32_t *pix_out;               // per sample (fused pixel writes): its pixel's output index
     uint32_t *batch_cost;           // chain launch: per 64-sample batch, its wave's duration (100 MHz ticks)
     int32_t *batch_order;           // chain launch: dispatch order of the batches (cost descending), or unused
-    int32_t *order_scratch;         // counting-sort scratch (kOrderBuckets histogram + offsets)
+    int32_t *order_scratch;         // counting-sort scratch (kOrderKeys histogram + offsets)
     int64_t cap;                    // samples per batch
     int32_t steps;                  // chain steps allocated (max_lvl + 1)
 };
@@ -111,9 +111,8 @@ constexpr int kWqStride = 16;                // one 64-B line per segment counte
 constexpr int kWqSlot = 8 * kWqStride;       // eight segments (one per XCD) per launch
 
 // Launchers (all asynchronous on `stream`).
-// k_gen_primary also zeroes w.counters (then counter 0 = the batch's samples) and w.wq. fused (one
-// sample per pixel): the chain launch will write the pixels; records w.pix_out and writes the
-// pixels outside the frame.
+// k_gen_primary also zeroes w.counters (then counter 0 = the batch's samples) and w.wq. fused: the
+// chain launch will write the pixels; records w.pix_out and writes the pixels outside the frame.
 void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream, bool fused = false,
                         uint8_t *out_u8 = nullptr);
 void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevWork &w, hipStream_t stream);
@@ -124,17 +123,20 @@ void launch_shadow_hit(const DevScene &s, const DevWork &w, const ShadeParams &p
 void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int64_t capacity, hipStream_t stream);
 void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream);
 // Steps first..max_lvl of every query in Q_first in one launch (closest-hit, shadows, shade per lane).
-// out_u8/out_f32 (first == 0, after launch_gen_primary(fused)): each sample's pixel is written at
-// the end of its chain with k_frame's arithmetic, so no k_frame follows.
+// fuse_spp > 0 (first == 0, after launch_gen_primary(fused); fuse_spp = samples per pixel, a divisor
+// of 64): each wave writes its pixels into out_u8/out_f32 when its batch's chains end, with
+// k_frame's arithmetic, so no k_frame follows.
 void launch_chain(const DevScene &s, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
-                  hipStream_t stream, bool ordered = false, uint8_t *out_u8 = nullptr, float *out_f32 = nullptr);
+                  hipStream_t stream, bool ordered = false, uint8_t *out_u8 = nullptr, float *out_f32 = nullptr,
+                  int fuse_spp = 0);
 void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t stream);
 // Batch order: the chain launch's 64-sample batches sorted by the durations it measured, longest
 // first (w.batch_cost -> w.batch_order); the next launch over the same batches dispatches in that
 // order (launch_chain(..., ordered = true)). A counting sort: one fill and three small launches.
 constexpr int kOrderBuckets = 128;
+constexpr int kOrderKeys = 8 * kOrderBuckets;   // (XCD segment, duration bucket) keys (RT_TUNE_BATCH_ORDER 2)
 constexpr int kWaveBatch = 64;   // samples per wave batch of the chain launch (one per lane)
-void launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream);
+void launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream, bool xcd_segments = false);
 void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *dst, int32_t n,
                            int32_t *idx, float4 *I, hipStream_t stream);
 

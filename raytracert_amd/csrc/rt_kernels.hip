@@ -1381,8 +1381,7 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
 }
 
 // Also resets the batch's queue counters and work-queue slots (counter 0 = the queue's size), so
-// no separate fills precede the batch. fused (one sample per pixel; the chain launch writes the
-// pixels): also records each sample's pixel index in w.pix_out and writes the pixels outside the
+// no separate fills precede the batch. fused (the chain launch writes the pixels): also records each sample's pixel index in w.pix_out and writes the pixels outside the
 // frame black in the tile-major layout, as k_frame does.
 __global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWork w, uint8_t *__restrict__ fused_u8,
                                                         int fused) {
@@ -1397,11 +1396,11 @@ __global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWo
     const int subx = sub / g.pfy, suby = sub - subx * g.pfy;   // subx outer, suby inner (:377-378)
     int x, y;
     const bool valid = decode_pixel(g, pix, x, y);
-    if (fused) {   // (spp == 1: s == pix)
+    if (fused) {
         const int64_t px = g.out_mode == 0 ? static_cast<int64_t>(g.tile0) * g.tw * g.th + pix
                                            : static_cast<int64_t>(y - g.oy) * g.cw + (x - g.ox);
         if (valid) w.pix_out[s] = static_cast<int32_t>(px);
-        else if (g.out_mode == 0 && fused_u8) { fused_u8[3 * px] = 0; fused_u8[3 * px + 1] = 0; fused_u8[3 * px + 2] = 0; }
+        else if (g.out_mode == 0 && fused_u8 && sub == 0) { fused_u8[3 * px] = 0; fused_u8[3 * px + 1] = 0; fused_u8[3 * px + 2] = 0; }
     }
     V3 origin = mk(0, 0, 0), dest = mk(0, 0, 0);
     if (valid) {
@@ -1483,6 +1482,21 @@ struct Secondary {
     V3 org, dst;
     int lvl;
 };
+
+// A chain record store. RT_CHAIN_SC1 (A/B build): written through past L2 (sc1), so the records,
+// read back once when the chain is folded, do not evict scene lines from the XCD's L2.
+#ifndef RT_CHAIN_SC1
+#define RT_CHAIN_SC1 1   // measured ~1.5% faster C4 frame (0.520 vs 0.528 ms)
+#endif
+__device__ __forceinline__ void store_chain(float4 *p, float4 v) {
+    if (RT_CHAIN_SC1) {
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        const f4 x = {v.x, v.y, v.z, v.w};
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(x) : "memory");
+    } else {
+        *p = v;
+    }
+}
 
 // reflection (raytracing.cpp:277-285) + addOffset (:266-271): the traced ray of level `lvl`.
 __device__ __forceinline__ void reflection_ray(V3 ray, V3 p, V3 normal, V3 &point, V3 &dest) {
@@ -1595,15 +1609,15 @@ __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadePa
         sec.state = kChildTrace; sec.coef = Ks; sec.lvl = lvl + 1;
         reflection_ray(ray, P, normal, sec.org, sec.dst);
     }
-    w.chain_local[ci] = make_float4(color.x, color.y, color.z, as_float(static_cast<int>(sec.state)));
-    if (sec.state == kChildTrace) w.chain_coef[ci] = make_float4(sec.coef.x, sec.coef.y, sec.coef.z, 0.0f);
+    store_chain(&w.chain_local[ci], make_float4(color.x, color.y, color.z, as_float(static_cast<int>(sec.state))));
+    if (sec.state == kChildTrace) store_chain(&w.chain_coef[ci], make_float4(sec.coef.x, sec.coef.y, sec.coef.z, 0.0f));
     else w.depth[sample] = static_cast<uint8_t>(step + 1);
     return sec;
 }
 
 // trace() miss (:389-391): black, and the chain ends at this step.
 __device__ __forceinline__ void shade_miss(const DevWork &w, int step, int sample) {
-    w.chain_local[static_cast<int64_t>(step) * w.cap + sample] = make_float4(0, 0, 0, as_float(kChildNone));
+    store_chain(&w.chain_local[static_cast<int64_t>(step) * w.cap + sample], make_float4(0, 0, 0, as_float(kChildNone)));
     w.depth[sample] = static_cast<uint8_t>(step + 1);
 }
 
@@ -1748,7 +1762,7 @@ template <int W, bool kAnyHit, bool kCount>
 __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CHAIN_WPE))) void k_chain(
     const DevScene sc, const ShadeParams p, DevWork w, int first, const Bvh4Node *__restrict__ n4,
     const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx, int ordered, uint8_t *__restrict__ out_u8,
-    float *__restrict__ out_f32) {
+    float *__restrict__ out_f32, int fuse_spp) {
     extern __shared__ int32_t lds_stack[];
     __shared__ int s_q[kChainSteps], s_sh[kChainSteps];
     for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) { s_q[i] = 0; s_sh[i] = 0; }
@@ -1766,6 +1780,8 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
         const int vb = j0 >> 6;   // this wave's batch in dispatch order (wave-uniform when ordered)
         const int pb = (ordered && (vb << 6) < end) ? w.batch_order[vb] : vb;
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        V3 rgb = mk(0, 0, 0);   // fused pixels: this lane's folded chain and its pixel (valid samples)
+        int px = -1;
         [&](int j) {
         if (j >= end) return;
         if (sc.chain_split & 4) j = nq - 1 - j;   // (diagnostic: reversed order)
@@ -1786,12 +1802,17 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
             dst = sec.dst;
             lvl = sec.lvl;
         }
-        if (out_u8 || out_f32) {   // fused pixel (one sample per pixel): k_frame's fold, /1, clamp, quantise
-            V3 rgb = fold_chain(w, sample);
-            rgb = mk(rgb.x / 1.0f, rgb.y / 1.0f, rgb.z / 1.0f);   // operator/ by float(pf^2), Vec3D.h:36-38
-            store_pixel(rgb, 3 * static_cast<int64_t>(w.pix_out[sample]), out_u8, out_f32);
-        }
+        if (fuse_spp) { rgb = fold_chain(w, sample); px = w.pix_out[sample]; }
         }(ordered ? pb * kWave + (j0 & (kWave - 1)) : j0);
+        if (fuse_spp) {   // k_frame's arithmetic: a pixel's fuse_spp sub-samples sit in adjacent lanes
+            const int lane = __lane_id(), base = lane & ~(fuse_spp - 1);
+            V3 acc = mk(0, 0, 0);
+            for (int sub = 0; sub < fuse_spp; ++sub)   // summed in sub-sample order (main.cpp:377-391)
+                acc = add(acc, mk(__shfl(rgb.x, base + sub), __shfl(rgb.y, base + sub), __shfl(rgb.z, base + sub)));
+            const float div = static_cast<float>(fuse_spp);
+            acc = mk(acc.x / div, acc.y / div, acc.z / div);   // operator/, Vec3D.h:36-38
+            if (lane == base && px >= 0) store_pixel(acc, 3 * static_cast<int64_t>(px), out_u8, out_f32);
+        }
         if (__lane_id() == 0 && j0 < end)
             w.batch_cost[pb] = static_cast<uint32_t>(min(__builtin_amdgcn_s_memrealtime() - t0, 0xFFFFFFFFull));
     });
@@ -1855,42 +1876,74 @@ __device__ __forceinline__ int order_bucket(uint32_t c) {
     return kOrderBuckets - 1 - min(k, kOrderBuckets - 1);   // descending duration
 }
 
-__global__ __launch_bounds__(kOrderBlock) void k_order_hist(const uint32_t *__restrict__ cost, int n, int32_t *hist) {
-    __shared__ int h[kOrderBuckets];
-    for (int i = threadIdx.x; i < kOrderBuckets; i += kOrderBlock) h[i] = 0;
+// XCD segments (segs == kXcds): dispatch slot v runs on XCD (v / 2) % 8 (two wave batches per
+// block, blocks dealt round-robin to the XCDs), so XCD x owns seg_count(n, x) of the n slots.
+// Segment x is that many consecutive batches in screen order and the sort runs within each
+// segment: each XCD's L2 then holds the geometry of one band of the screen, and within the band
+// the longest batches go first. Placement only; results never change.
+__device__ __forceinline__ int seg_count(int n, int x) { return 2 * (n / 16) + min(2, max(0, n % 16 - 2 * x)); }
+__device__ __forceinline__ int seg_of(int n, int i, int &start) {
+    int x = 0;
+    start = 0;
+    while (x < kXcds - 1 && i >= start + seg_count(n, x)) { start += seg_count(n, x); ++x; }
+    return x;
+}
+
+__global__ __launch_bounds__(kOrderBlock) void k_order_hist(const uint32_t *__restrict__ cost, int n, int segs,
+                                                         int32_t *hist) {
+    __shared__ int h[kOrderKeys];
+    const int nk = segs * kOrderBuckets;
+    for (int i = threadIdx.x; i < nk; i += kOrderBlock) h[i] = 0;
     __syncthreads();
-    for (int i = blockIdx.x * kOrderBlock + threadIdx.x; i < n; i += gridDim.x * kOrderBlock) atomicAdd(&h[order_bucket(cost[i])], 1);
+    for (int i = blockIdx.x * kOrderBlock + threadIdx.x; i < n; i += gridDim.x * kOrderBlock) {
+        int start = 0;
+        const int x = segs > 1 ? seg_of(n, i, start) : 0;
+        atomicAdd(&h[x * kOrderBuckets + order_bucket(cost[i])], 1);
+    }
     __syncthreads();
-    for (int i = threadIdx.x; i < kOrderBuckets; i += kOrderBlock)
+    for (int i = threadIdx.x; i < nk; i += kOrderBlock)
         if (h[i]) atomicAdd(&hist[i], h[i]);
 }
 
-__global__ __launch_bounds__(kOrderBuckets) void k_order_scan(int32_t *hist) {
-    __shared__ int h[kOrderBuckets];
-    h[threadIdx.x] = hist[threadIdx.x];
+__global__ __launch_bounds__(kOrderKeys) void k_order_scan(int32_t *hist, int nk) {
+    __shared__ int h[kOrderKeys];
+    if (static_cast<int>(threadIdx.x) < nk) h[threadIdx.x] = hist[threadIdx.x];
     __syncthreads();
     if (threadIdx.x == 0) {
         int acc = 0;
-        for (int i = 0; i < kOrderBuckets; ++i) { const int c = h[i]; h[i] = acc; acc += c; }
+        for (int i = 0; i < nk; ++i) { const int c = h[i]; h[i] = acc; acc += c; }
     }
     __syncthreads();
-    hist[threadIdx.x] = h[threadIdx.x];   // bucket offsets; the scatter advances them
+    if (static_cast<int>(threadIdx.x) < nk) hist[threadIdx.x] = h[threadIdx.x];   // key offsets; the scatter advances them
 }
 
-__global__ __launch_bounds__(kOrderBlock) void k_order_scatter(const uint32_t *__restrict__ cost, int n, int32_t *offs,
-                                                            int32_t *__restrict__ order) {
-    __shared__ int h[kOrderBuckets], base[kOrderBuckets];
+__global__ __launch_bounds__(kOrderBlock) void k_order_scatter(const uint32_t *__restrict__ cost, int n, int segs,
+                                                            int32_t *offs, int32_t *__restrict__ order) {
+    __shared__ int h[kOrderKeys], base[kOrderKeys];
+    const int nk = segs * kOrderBuckets;
     for (int i0 = blockIdx.x * kOrderBlock; i0 < n; i0 += gridDim.x * kOrderBlock) {   // block-uniform
-        for (int i = threadIdx.x; i < kOrderBuckets; i += kOrderBlock) h[i] = 0;
+        for (int i = threadIdx.x; i < nk; i += kOrderBlock) h[i] = 0;
         __syncthreads();
         const int i = i0 + static_cast<int>(threadIdx.x);
-        int b = 0, r = 0;
-        if (i < n) { b = order_bucket(cost[i]); r = atomicAdd(&h[b], 1); }
+        int b = 0, r = 0, x = 0, start = 0;
+        if (i < n) {
+            x = segs > 1 ? seg_of(n, i, start) : 0;
+            b = x * kOrderBuckets + order_bucket(cost[i]);
+            r = atomicAdd(&h[b], 1);
+        }
         __syncthreads();
-        for (int k = threadIdx.x; k < kOrderBuckets; k += kOrderBlock)
+        for (int k = threadIdx.x; k < nk; k += kOrderBlock)
             if (h[k]) base[k] = atomicAdd(&offs[k], h[k]);
         __syncthreads();
-        if (i < n) order[base[b] + r] = i;
+        if (i < n) {
+            const int pos = base[b] + r;
+            if (segs > 1) {   // rank within the segment -> the slot of that rank on the segment's XCD
+                const int rk = pos - start;
+                order[2 * (x + kXcds * (rk >> 1)) + (rk & 1)] = i;
+            } else {
+                order[pos] = i;
+            }
+        }
         __syncthreads();
     }
 }
@@ -2019,7 +2072,7 @@ void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int
 }
 
 void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
-                  hipStream_t stream, bool ordered, uint8_t *out_u8, float *out_f32) {
+                  hipStream_t stream, bool ordered, uint8_t *out_u8, float *out_f32, int fuse_spp) {
     if (capacity <= 0) return;
     const bool wide = tree_variant(s0, -1) == 4;
     const DevScene s = for_width(s0, wide ? 4 : 2);
@@ -2031,7 +2084,7 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
                  : (s.any_transparent ? k_chain<2, false, true> : k_chain<2, true, true>);
 #endif
     hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, p, w, first,
-                       s.nodes4, s.leaf_recs, s.leaf_idx, ordered ? 1 : 0, out_u8, out_f32);
+                       s.nodes4, s.leaf_recs, s.leaf_idx, ordered ? 1 : 0, out_u8, out_f32, fuse_spp);
 }
 
 void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream) {
@@ -2040,15 +2093,16 @@ void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *
     hipLaunchKernelGGL(k_frame, dim3(grid_for(n)), dim3(kBlock), 0, stream, g, w, out_u8, out_f32);
 }
 
-void launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream) {
+void launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream, bool xcd_segments) {
     if (nbatches <= 0) return;
     const int n = static_cast<int>(nbatches);
-    hipMemsetAsync(w.order_scratch, 0, sizeof(int32_t) * kOrderBuckets, stream);
+    const int segs = xcd_segments ? kXcds : 1, nk = segs * kOrderBuckets;
+    hipMemsetAsync(w.order_scratch, 0, sizeof(int32_t) * nk, stream);
     const unsigned grid = static_cast<unsigned>(std::min<int64_t>((nbatches + kOrderBlock - 1) / kOrderBlock, 1024));
-    hipLaunchKernelGGL(k_order_hist, dim3(grid), dim3(kOrderBlock), 0, stream, w.batch_cost, n, w.order_scratch);
-    hipLaunchKernelGGL(k_order_scan, dim3(1), dim3(kOrderBuckets), 0, stream, w.order_scratch);
-    hipLaunchKernelGGL(k_order_scatter, dim3(grid), dim3(kOrderBlock), 0, stream, w.batch_cost, n, w.order_scratch,
-                       w.batch_order);
+    hipLaunchKernelGGL(k_order_hist, dim3(grid), dim3(kOrderBlock), 0, stream, w.batch_cost, n, segs, w.order_scratch);
+    hipLaunchKernelGGL(k_order_scan, dim3(1), dim3(kOrderKeys), 0, stream, w.order_scratch, nk);
+    hipLaunchKernelGGL(k_order_scatter, dim3(grid), dim3(kOrderBlock), 0, stream, w.batch_cost, n, segs,
+                       w.order_scratch, w.batch_order);
 }
 
 void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t stream) {

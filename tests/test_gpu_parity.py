@@ -164,16 +164,19 @@ def test_frame_device_equals_rectangle_render(size, pf, workdir, gpu_available):
             assert [int(x) for x in c] == [int(x) for x in counts]
 
 
-@pytest.mark.parametrize("spec,size,want_f32", [("syn:F3", (100, 70), True), ("syn:C4", (1920, 1080), False),
-                                                 ("syn:F4", (37, 23), True)])
-def test_fused_pixel_writes_equal_frame_pass(spec, size, want_f32, workdir, gpu_available):
-    """RT_TUNE_FUSE_PIXELS: with one sample per pixel the chain launch writes each pixel when its
-    chain ends. Bytes, floats and ray counts equal the separate frame pass's, for the rectangle
-    render, the whole-frame device render and the tile-major shard layout (whose pixels outside
-    the frame are written black: ragged sizes leave partial tiles)."""
+@pytest.mark.parametrize("spec,size,pf,want_f32", [("syn:F3", (100, 70), 1, True), ("syn:C4", (1920, 1080), 1, False),
+                                                    ("syn:F4", (37, 23), 1, True), ("syn:F3", (100, 70), 2, True),
+                                                    ("syn:F4", (37, 23), 4, True), ("syn:F3", (61, 29), 3, True),
+                                                    ("syn:C4", (640, 360), 2, False)])
+def test_fused_pixel_writes_equal_frame_pass(spec, size, pf, want_f32, workdir, gpu_available):
+    """RT_TUNE_FUSE_PIXELS: the chain launch writes each pixel when its samples' chains end (the
+    pf^2 sub-samples summed across adjacent lanes in k_frame's order; pf 3 does not divide a batch
+    and keeps the frame pass). Bytes, floats and ray counts equal the separate frame pass's, for
+    the rectangle render, the whole-frame device render and the tile-major shard layout (whose
+    pixels outside the frame are written black: ragged sizes leave partial tiles)."""
     import torch
     w, h = size
-    p = R.RenderParams(width=w, height=h, pf=1, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
+    p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
     ntiles = ((w + 15) // 16) * ((h + 15) // 16)
     out = {}
     with R.Scene.load(scene_path(spec, workdir), device=0) as sc:
@@ -319,15 +322,18 @@ def test_c4_full_frame_bvh_equals_brute_force(workdir, gpu_available):
         assert np.array_equal(xf.view(np.uint32), bf.view(np.uint32))
 
 
-def test_batch_order_from_previous_launch_keeps_results(workdir, gpu_available):
+@pytest.mark.parametrize("mode,pf,size", [(1, 1, (320, 180)), (2, 1, (320, 180)), (2, 2, (200, 110)),
+                                          (2, 1, (37, 23))])
+def test_batch_order_from_previous_launch_keeps_results(mode, pf, size, workdir, gpu_available):
     """RT_TUNE_BATCH_ORDER: the first render dispatches the chain's batches in screen order and
-    times them; the next renders over the same batches dispatch them longest first. Every render
-    is byte-identical with identical ray counts, with the order on or off."""
-    p = R.RenderParams(width=320, height=180, pf=1, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
+    times them; the next renders over the same batches dispatch them longest first (mode 2: within
+    one screen band per XCD, including frames of fewer than 16 batches). Every render is
+    byte-identical with identical ray counts, with the order on or off."""
+    p = R.RenderParams(width=size[0], height=size[1], pf=pf, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
     with R.Scene.load(scene_path("syn:C4", workdir), device=0) as sc:
         sc.tune("batch_order", 0)
         ref, fref, cref = sc.render(p, want_f32=True)
-        sc.tune("batch_order", 1)
+        sc.tune("batch_order", mode)
         sc.tune("order_every", 2)
         for _ in range(5):
             u8, f32, counts = sc.render(p, want_f32=True)
@@ -373,7 +379,8 @@ def test_multi_frame_shard_batch_reassembles(workdir, gpu_available):
                                    {"chain_from": 3}, {"chain_from": 255}, {"chain_from": 0, "lds_stack": 1},
                                    {"chain_from": 1, "bvh_width": 2}, {"chain_from": 0, "pipes": 1},
                                    {"pipes": 2}, {"pipes": 2, "bvh_grid": 4096}, {"bvh_grid": 65536},
-                                   {"fuse_pixels": 0}])
+                                   {"fuse_pixels": 0}, {"batch_order": 2}, {"batch_order": 2, "chain_split": 3},
+                                   {"chain_split": 1}, {"chain_split": 2}])
 def test_launch_shape_knobs_never_change_results(knobs, workdir, gpu_available):
     """Query distribution (grid-stride, static XCD segments, work-stealing XCD queues), tiny grids
     (fewer blocks than XCDs), tree width and the LDS/HBM split of the traversal stack (1 entry in
