@@ -30,28 +30,34 @@ sys.path.insert(0, HERE)
 METRIC = "Mrays/s + wall-clock per frame at 1920×1080, 100k-tri OBJ"
 FLOP_PER_TEST = 37            # fp32 ops of rayIntersectTriangle's dominant path
 FLOP_PER_NODE = 52            # BVH node visit: 2 slab tests (6 sub + 6 mul + 12 min/max each) + 2 distance culls
-FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector (= FP32 matrix) peak
+FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector (= FP32 matrix) peak (packed FMA)
+# The same issue rate without packing (x2) or FMA (x2), which parity forbids for the triangle test:
+# 256 CUs x 64 lanes x 2.4 GHz x 1 flop = 39.3 TFLOP/s (the brute-force kernel's practical ceiling)
+FP32_NOFMA_NOPACK_TFLOPS = 39.3
 HBM_PEAK_GBS = 8000.0
 TILE = 16
 # BASELINE.json configs. C4 is the metric's configuration and the default; the
 # others are available with --workload (C1 is the reference's own CPU-only plumbing case).
 WORKLOADS = {
     "c4": dict(desc="C4: synthetic 8x8 UV-sphere grid OBJ (102,402 tris) 1920x1080, pf 1, depth 3, 2 lights",
-               scene="syn:C4", width=1920, height=1080, pf=1, max_lvl=3, lights=((0.0, 0.0, 4.0), (1.5, 1.5, 4.0))),
+               scene="syn:C4", width=1920, height=1080, pf=1, max_lvl=3, lights=((0.0, 0.0, 4.0), (1.5, 1.5, 4.0)),
+               cpu_every=96),
     "c2": dict(desc="C2: dodgeColorTest.obj (16,311 tris) 800x600, pf 1, depth 1, 1 light",
-               scene="ref:dodgeColorTest.obj", width=800, height=600, pf=1, max_lvl=1, lights=((0.0, 0.0, 4.0),)),
+               scene="ref:dodgeColorTest.obj", width=800, height=600, pf=1, max_lvl=1, lights=((0.0, 0.0, 4.0),),
+               cpu_every=1),
     "c3": dict(desc="C3: Balls surrogate (3 UV spheres 48x24 + ground quad, Balls.mtl materials) 1920x1080, pf 1, "
                     "depth 3, 2 lights (Balls.obj is missing from the reference)",
-               scene="syn:balls", width=1920, height=1080, pf=1, max_lvl=3, lights=((0.0, 0.0, 4.0), (2.0, 2.0, 4.0))),
+               scene="syn:balls", width=1920, height=1080, pf=1, max_lvl=3, lights=((0.0, 0.0, 4.0), (2.0, 2.0, 4.0)),
+               cpu_every=16),
     "c5": dict(desc="C5: synthetic 16x16 UV-sphere grid OBJ (1,015,810 tris) 3840x2160, pf 2 (4 samples/pixel, "
                     "the reference's regular AA grid), depth 3, 4 lights",
                scene="syn:C5", width=3840, height=2160, pf=2, max_lvl=3,
-               lights=((0.0, 0.0, 4.0), (1.5, 1.5, 4.0), (-1.5, 1.5, 4.0), (0.0, -1.5, 4.0))),
+               lights=((0.0, 0.0, 4.0), (1.5, 1.5, 4.0), (-1.5, 1.5, 4.0), (0.0, -1.5, 4.0)), cpu_every=1024),
     "c5s": dict(desc="C5 stochastic: synthetic 16x16 UV-sphere grid OBJ (1,015,810 tris) 3840x2160, 4 jittered "
                      "samples/pixel (RT_STOCHASTIC, seed 0x5EED: pf 2 strata, counter-hash jitter; an extension of "
                      "the reference's regular grid), depth 3, 4 lights",
                 scene="syn:C5", width=3840, height=2160, pf=2, max_lvl=3, stochastic=True,
-                lights=((0.0, 0.0, 4.0), (1.5, 1.5, 4.0), (-1.5, 1.5, 4.0), (0.0, -1.5, 4.0))),
+                lights=((0.0, 0.0, 4.0), (1.5, 1.5, 4.0), (-1.5, 1.5, 4.0), (0.0, -1.5, 4.0)), cpu_every=1024),
 }
 
 
@@ -76,8 +82,14 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mode", choices=("weak", "strong"), default="weak")
-    ap.add_argument("--cpu-sample-every", type=int, default=96, help="CPU baseline: every k-th tile")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-sample-every", type=int, default=0,
+                    help="CPU baseline: every k-th tile (0: the workload's default, C2 the full frame)")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="the GPU box's CPU share (16 per GPU)")
+    ap.add_argument("--cpu-single-budget", type=float, default=15.0,
+                    help="1-thread CPU figure: seconds spent on 4x4-pixel blocks of the sampled tiles")
+    ap.add_argument("--no-cold", action="store_true", help="skip the cold (unordered) first-frame measurement")
+    ap.add_argument("--no-path-compare", action="store_true",
+                    help="N=1: skip timing the shard path (tiles + un-permute) beside the frame path")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=1, help="steps re-run with HIP events for the roofline")
     ap.add_argument("--ppm", default="", help="write the first frame to this PPM (rank 0)")
@@ -136,90 +148,139 @@ def main():
     cparams = params.to_c()
 
     layout = rdist.TileLayout(WIDTH, HEIGHT, TILE, TILE)
-    plan = rdist.ShardPlan(layout, world, frames=world if args.mode == "weak" else 1)
-    # two shard buffers: step i renders into bufs[i % 2] while step i-1's gather reads the other
-    bufs = [torch.zeros(plan.shard_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
-    index = torch.as_tensor(plan.gather_index(), device=dev)
     stream = torch.cuda.current_stream(dev)
 
-    def render_shard(want_counts=False, buf=None):
-        # one call: this rank's tile ids rank, rank + N, ... over the step's `frames` frames
-        buf = bufs[0] if buf is None else buf
-        n, c = scene.render_tiles_device(cparams, TILE, TILE, rank, world, buf.data_ptr(), buf.numel(),
-                                         stream.cuda_stream, want_counts=want_counts, frames=plan.frames)
-        assert n == plan.rank_tiles(rank)
-        return c if c is not None else np.zeros(3, np.uint64)
+    class Runner:
+        """One way of rendering a step. frames: frames per step (weak: N, strong: 1); frame_path:
+        one GPU writes the row-major frame itself (rt_render_frame_device: no gather, no
+        un-permute); otherwise every rank renders its interleaved tiles (rt_render_tiles_device),
+        rank 0 gathers them (one RCCL gather) and un-permutes them on the device."""
 
-    pending = []
+        def __init__(self, frames, frame_path):
+            self.plan = rdist.ShardPlan(layout, world, frames=frames)
+            self.single = frame_path
+            # two buffers: step i renders into bufs[i % 2] while step i-1's gather reads the other
+            self.bufs = [torch.zeros(self.plan.shard_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
+            self.index = torch.as_tensor(self.plan.gather_index(), device=dev)
+            if frame_path:
+                self.fbufs = [torch.zeros(HEIGHT * WIDTH * 3, dtype=torch.uint8, device=dev) for _ in range(2)]
+            self.pending = []
 
-    def finish(p):
-        # order the stream after the gather, then un-permute on rank 0
-        if p is None:
-            return None
-        gathered, work = p
-        if work is not None:
-            work.wait()
-        return rdist.assemble_plan_torch(gathered, plan, index) if rank == 0 else None
+        def render_shard(self, want_counts=False, buf=None):
+            # one call: this rank's tile ids rank, rank + N, ... over the step's `frames` frames
+            buf = self.bufs[0] if buf is None else buf
+            n, c = scene.render_tiles_device(cparams, TILE, TILE, rank, world, buf.data_ptr(), buf.numel(),
+                                             stream.cuda_stream, want_counts=want_counts, frames=self.plan.frames)
+            assert n == self.plan.rank_tiles(rank)
+            return c if c is not None else np.zeros(3, np.uint64)
 
-    single = world == 1 and plan.frames == 1
-    if single:   # one GPU: the library writes the row-major frame itself (no gather, no un-permute)
-        fbufs = [torch.zeros(HEIGHT * WIDTH * 3, dtype=torch.uint8, device=dev) for _ in range(2)]
+        def render_once(self, i=0):
+            """The step's render call alone (the roofline's profiled launches use this)."""
+            if self.single:
+                fb = self.fbufs[i % 2]
+                scene.render_frame_device(cparams, TILE, TILE, fb.data_ptr(), fb.numel(), stream.cuda_stream)
+                return fb
+            return self.render_shard(buf=self.bufs[i % 2])
 
-    def step(i):
-        """Render step i's shard, start its gather (async, on the collective's stream) and finish
-        step i-1's: the gather of one step overlaps the next step's render."""
-        if single:
-            fb = fbufs[i % 2]
-            scene.render_frame_device(cparams, TILE, TILE, fb.data_ptr(), fb.numel(), stream.cuda_stream)
-            return fb.view(1, HEIGHT, WIDTH, 3)
-        render_shard(buf=bufs[i % 2])
-        pending.append(rdist.gather_shards(bufs[i % 2], rank, world, async_op=True))
-        return finish(pending.pop(0)) if len(pending) > 1 else None
+        def finish(self, p):
+            # order the stream after the gather, then un-permute on rank 0
+            gathered, work = p
+            if work is not None:
+                work.wait()
+            return rdist.assemble_plan_torch(gathered, self.plan, self.index) if rank == 0 else None
 
-    def drain():
-        return finish(pending.pop(0)) if pending else None
+        def step(self, i):
+            """Render step i, start its gather (async, on the collective's stream) and finish step
+            i-1's: the gather of one step overlaps the next step's render."""
+            if self.single:
+                return self.render_once(i).view(1, HEIGHT, WIDTH, 3)
+            self.render_shard(buf=self.bufs[i % 2])
+            self.pending.append(rdist.gather_shards(self.bufs[i % 2], rank, world, async_op=True))
+            return self.finish(self.pending.pop(0)) if len(self.pending) > 1 else None
+
+        def drain(self):
+            return self.finish(self.pending.pop(0)) if self.pending else None
+
+        def run(self, steps, warmup):
+            """warmup untimed steps, then `steps` timed ones between barriers + device syncs;
+            returns (max-over-ranks seconds, last frames)."""
+            for i in range(warmup):
+                self.step(i)
+            self.drain()
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            frames = None
+            for i in range(steps):
+                f = self.step(i)
+                frames = f if f is not None else frames
+            f = self.drain()   # the last step's gather + un-permute stay inside the timed region
+            frames = f if f is not None else frames
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+            if world > 1:
+                dist.all_reduce(el, op=dist.ReduceOp.MAX)
+            return float(el.item()), frames
+
+    main_run = Runner(world if args.mode == "weak" else 1, frame_path=world == 1)
+    plan = main_run.plan
 
     # rays per step (deterministic): counted once, summed over ranks
-    counts = render_shard(want_counts=True)
+    counts = main_run.render_shard(want_counts=True)
     ct = torch.tensor([int(c) for c in counts], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(ct)
     rays_per_step = float(ct.sum().item())
     rays_by_kind = [int(x) for x in ct.tolist()]
 
-    for i in range(args.warmup):
-        step(i)
-    drain()
-    torch.cuda.synchronize(dev)
+    # ---- timed region (the metric) ----
+    elapsed, frames = main_run.run(args.steps, args.warmup)
 
-    # ---- timed region ----
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    frames = None
-    for i in range(args.steps):
-        f = step(i)
-        frames = f if f is not None else frames
-    f = drain()   # the last step's gather + un-permute stay inside the timed region
-    frames = f if f is not None else frames
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+    # ---- a cold frame: no measured batch order yet (the first frame of a new view) ----
+    scene.tune("batch_order", 0)   # screen-order dispatch, exactly what a view's first launch does
+    cold = []
+    for i in range(0 if args.no_cold else 3):
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        main_run.step(i)
+        main_run.drain()
+        torch.cuda.synchronize(dev)
+        cold.append(time.perf_counter() - t0)
+    scene.tune("batch_order", 1)
+    cold_ms = sorted(cold)[1] * 1e3 if cold else None
+
+    # ---- the same work through the other path: N=1 the shard path (tiles + un-permute, what
+    # N>1 runs, minus the collective); N>1 strong scaling (one frame split over the ranks) ----
+    extra = {}
+    if world == 1 and not args.no_path_compare and args.accel == "bvh":
+        el2, _ = Runner(1, frame_path=False).run(args.steps, max(args.warmup, 2))
+        extra["shard_path"] = {"what": "rt_render_tiles_device (interleaved 16x16 tiles) + device un-permute, "
+                                       "the N>1 step without its gather", "ms_per_step": round(el2 / args.steps * 1e3, 3),
+                               "value": round(rays_per_step * args.steps / el2 / 1e6, 4)}
+    if world > 1 and args.mode == "weak":
+        srun = Runner(1, frame_path=False)
+        el2, _ = srun.run(args.steps, max(args.warmup, 2))
+        extra["strong"] = {"what": "one frame split over the N ranks per step (strong scaling)",
+                           "ms_per_frame": round(el2 / args.steps * 1e3, 3),
+                           "value": round(rays_per_step / world * args.steps / el2 / 1e6, 4)}
 
     # ---- kernel timing for the roofline (HIP events on the scene's launch stream) ----
-    def profile(steps):
-        # kernel durations in isolation: one pipeline, so no launch shares the GPU with another
+    def profile(steps, runner):
+        # kernel durations in isolation: one pipeline, so no launch shares the GPU with another;
+        # the same entry point as the timed loop, after it (so every launch is batch-ordered)
         scene.tune("pipes", 1)
+        runner.render_once()
+        torch.cuda.synchronize(dev)
         scene.reset_stats()
         scene.set_profiling(True)
-        for _ in range(max(steps, 1)):
-            render_shard()
+        for i in range(max(steps, 1)):
+            runner.render_once(i)
         torch.cuda.synchronize(dev)
         scene.set_profiling(False)
         st = {k: scene.kernel_stats(k) for k in (KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME, KERNEL_CHAIN)}
@@ -227,15 +288,15 @@ def main():
         if scene.accel() == "bvh":   # work counters slow the kernels: count in a separate, untimed pass
             scene.reset_stats()
             scene.set_profiling(True, count_work=True)
-            for _ in range(max(steps, 1)):
-                render_shard()
+            for i in range(max(steps, 1)):
+                runner.render_once(i)
             torch.cuda.synchronize(dev)
             scene.set_profiling(False)
             work = scene.work_stats(KERNEL_CLOSEST_HIT) + scene.work_stats(KERNEL_SHADOW)
         scene.tune("pipes", args.pipes)
         return st, work
 
-    stats, (bvh_tests, bvh_visits, sh_bvh_tests, sh_bvh_visits) = profile(args.profile_steps)
+    stats, (bvh_tests, bvh_visits, sh_bvh_tests, sh_bvh_visits) = profile(args.profile_steps, main_run)
     chain_launches, chain_ms, chain_tests = stats[KERNEL_CHAIN]
     ch_launches, ch_ms, ch_tests = stats[KERNEL_CLOSEST_HIT]
     sh_launches, sh_ms, sh_tests = stats[KERNEL_SHADOW]
@@ -244,12 +305,15 @@ def main():
     bf = None
     if args.accel == "bvh" and not args.no_bf_roofline and rank == 0:
         scene.set_accel("brute_force")
-        bst, _ = profile(1)
+        bst, _ = profile(1, main_run if world == 1 else Runner(1, frame_path=False))
         scene.set_accel("bvh")
         l, ms, tests = bst[KERNEL_CLOSEST_HIT]
+        t = tests * FLOP_PER_TEST / (ms / 1e3) / 1e12
         bf = {"kernel": "k_closest_hit (brute force, --accel brute_force)", "bound": "valu",
-              "achieved": round(tests * FLOP_PER_TEST / (ms / 1e3) / 1e12, 3), "peak": FP32_PEAK_TFLOPS,
-              "unit": "TFLOP/s", "frac": round(tests * FLOP_PER_TEST / (ms / 1e3) / 1e12 / FP32_PEAK_TFLOPS, 4),
+              "achieved": round(t, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(t / FP32_PEAK_TFLOPS, 4),
+              "peak_no_fma_no_pack": FP32_NOFMA_NOPACK_TFLOPS, "frac_no_fma_no_pack": round(t / FP32_NOFMA_NOPACK_TFLOPS, 4),
+              "note": "parity forbids FMA contraction (the x86 reference has none), so the packed-FMA peak is "
+                      "unreachable; the no-FMA, non-packed issue rate is the practical ceiling",
               "launches": l, "avg_launch_ms": round(ms / max(l, 1), 3), "frame_closest_hit_ms": round(ms, 3)}
 
     result = None
@@ -257,42 +321,42 @@ def main():
         total_rays = rays_per_step * args.steps
         value = total_rays / elapsed / 1e6
         queries = ch_tests / max(nt, 1)
+        per_rank_steps = args.profile_steps
+        traffic = traffic_src = None
         if args.accel == "bvh" and chain_launches > 0:
-            # The chain kernel (every step of every sample per lane, RT_TUNE_CHAIN_FROM 0): per
-            # primary query 32 B in, per closest-hit query a 32-B chain record out, plus one 64-B
-            # record per node visit and per triangle test of its closest-hit and shadow queries
-            # (device counters). Roof: memory (HBM peak).
+            # The chain kernel (every step of every sample per lane, RT_TUNE_CHAIN_FROM 0). Roof:
+            # FP32 VALU at 37 flop per ray-triangle test and 52 per four-wide node
+            # visit (device work counters). Logical (L1-side) bytes: 32 B per primary query in, a
+            # 32-B chain record per closest-hit query, 64 B per node visit and per triangle test.
             kname = "k_chain"
             ch_launches, ch_ms = chain_launches, chain_ms   # the roofline's kernel from here on
-            queries = rays_by_kind[0] / world * args.profile_steps
+            queries = rays_by_kind[0] / world * per_rank_steps
             tests_all, visits_all = bvh_tests + sh_bvh_tests, bvh_visits + sh_bvh_visits
             flops = tests_all * FLOP_PER_TEST + visits_all * FLOP_PER_NODE
-            ch_bytes = (queries * 32.0 + (rays_by_kind[0] + rays_by_kind[1]) / world * args.profile_steps * 32.0 +
-                        (visits_all + tests_all) * 64.0)
+            logical = (queries * 32.0 + (rays_by_kind[0] + rays_by_kind[1]) / world * per_rank_steps * 32.0 +
+                       (visits_all + tests_all) * 64.0)
             bvh_tests, bvh_visits = tests_all, visits_all
             ch_tests = chain_tests
-            bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
-            achieved = ch_bytes / (ch_ms / 1e3) / 1e9 if ch_ms > 0 else 0.0
-            valu = flops / (ch_ms / 1e3) / 1e12 if ch_ms > 0 else 0.0
         elif args.accel == "bvh":
-            # BVH traversal is a dependent gather: per query 32 B in + 20 B out, plus one 64-B
-            # record per node visit and per triangle test (device counters). Roof: memory (HBM peak).
             kname = "k_bvh_closest_hit"
             flops = bvh_tests * FLOP_PER_TEST + bvh_visits * FLOP_PER_NODE
-            ch_bytes = queries * 52.0 + (bvh_visits + bvh_tests) * 64.0
-            bound, unit, peak = "hbm", "GB/s", HBM_PEAK_GBS
-            achieved = ch_bytes / (ch_ms / 1e3) / 1e9 if ch_ms > 0 else 0.0
-            valu = flops / (ch_ms / 1e3) / 1e12 if ch_ms > 0 else 0.0
+            logical = queries * 52.0 + (bvh_visits + bvh_tests) * 64.0
         else:
-            # brute force: each wave streams every 64-B record once (scalar loads); VALU-bound
             kname = "k_closest_hit"
             flops = ch_tests * FLOP_PER_TEST
-            ch_bytes = ch_tests / 64.0 * 64.0 + queries * 52.0
-            bound, unit, peak = "valu", "TFLOP/s", FP32_PEAK_TFLOPS
-            achieved = flops / (ch_ms / 1e3) / 1e12 if ch_ms > 0 else 0.0
-            valu = achieved
+            logical = ch_tests / 64.0 * 64.0 + queries * 52.0
+        avg_s = ch_ms / 1e3 / max(ch_launches, 1)
+        achieved = flops / max(ch_launches, 1) / avg_s / 1e12 if avg_s > 0 else 0.0
         # the committed PMC summary profiles the default workload (C4): other workloads carry none
-        traffic, traffic_src = pmc_traffic(kname) if args.workload == "c4" else (None, None)
+        if args.workload == "c4" and args.accel == "bvh":
+            traffic, traffic_src = pmc_traffic(kname)
+        dram = None
+        if traffic and avg_s > 0:
+            dram = {"achieved": round(traffic / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4),
+                    "bytes_per_launch": traffic, "source": traffic_src,
+                    "what": "bytes past the XCD L2s (PMC 2*FETCH_SIZE + WRITE_SIZE, gfx950 correction) / "
+                            "average launch time; Infinity Cache hits are included"}
         result = {
             "metric": METRIC,
             "value": round(value, 4),
@@ -312,31 +376,37 @@ def main():
                 "width": WIDTH, "height": HEIGHT, "pf": PF, "max_lvl": MAX_LVL, "lights": [list(l) for l in LIGHTS],
                 "triangles": nt, "vertices": nv, "tile": TILE,
                 "parallelism": f"tile-shard{world}",
+                "path": "rt_render_frame_device" if main_run.single else "rt_render_tiles_device + RCCL gather + un-permute",
                 "rays_per_step": int(rays_per_step),
                 "rays_by_kind_per_step": {"primary": rays_by_kind[0], "secondary": rays_by_kind[1], "shadow": rays_by_kind[2]},
                 "frame_ms_per_gpu": round(elapsed / args.steps * 1e3, 3),
+                "first_frame_ms": round(cold_ms, 3) if cold_ms is not None else None,
+                "first_frame_what": "a frame with no measured batch order (screen-order dispatch, as a new view's "
+                                    "first launch), median of 3, synchronised",
                 "scene_load_s": round(t_load, 3), "scene_gen_s": round(t_gen, 3),
             },
             "roofline": {
                 "kernel": f"{kname} ({'every chain step: closest-hit, shadow and shade' if kname == 'k_chain' else 'primary + secondary queries'}, accel={args.accel})",
-                "bound": bound,
+                "bound": "valu",
                 "achieved": round(achieved, 3),
-                "peak": peak,
-                "unit": unit,
-                "frac": round(achieved / peak, 4),
-                "algorithmic_bytes_per_launch": round(ch_bytes / max(ch_launches, 1)),
-                "valu_TFLOPs": round(valu, 3),
-                "valu_frac": round(valu / FP32_PEAK_TFLOPS, 4),
+                "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                 "traffic": traffic,
                 "traffic_unit": "bytes/launch (PMC: 2*FETCH_SIZE + WRITE_SIZE)",
-                "traffic_source": traffic_src,
-                "launches": ch_launches,
-                "avg_launch_ms": round(ch_ms / max(ch_launches, 1), 3),
-                "queries_per_launch": round(queries / max(ch_launches, 1)),
-                "tests_per_launch": round((bvh_tests if args.accel == "bvh" else ch_tests) / max(ch_launches, 1)),
-                "node_visits_per_launch": round(bvh_visits / max(ch_launches, 1)) if args.accel == "bvh" else 0,
+                "flop_per_launch": round(flops / max(ch_launches, 1)),
                 "flop_per_test": FLOP_PER_TEST,
                 "flop_per_node_visit": FLOP_PER_NODE,
+                "tests_per_launch": round((bvh_tests if args.accel == "bvh" else ch_tests) / max(ch_launches, 1)),
+                "node_visits_per_launch": round(bvh_visits / max(ch_launches, 1)) if args.accel == "bvh" else 0,
+                "queries_per_launch": round(queries / max(ch_launches, 1)),
+                "launches": ch_launches,
+                "avg_launch_ms": round(avg_s * 1e3, 4),
+                "timing": "HIP events on the launch stream, batch-ordered launches of the timed entry point only",
+                "dram": dram,
+                "logical_bytes_per_launch": round(logical / max(ch_launches, 1)),
+                "logical_bytes_what": "L1-side accesses (64 B per node visit and per triangle test, 32 B per query "
+                                      "in and per chain record out); most are served by L1/L2, so this is not HBM traffic",
                 "bruteforce_equivalent_TFLOPs": round(ch_tests * FLOP_PER_TEST / (ch_ms / 1e3) / 1e12, 3) if ch_ms > 0 else None,
             },
             "kernel_ms_per_step": {
@@ -350,6 +420,7 @@ def main():
             "accel": {"mode": args.accel, "bvh": bvh_info},
             "cpu_baseline": None,
         }
+        result.update(extra)
         if args.ppm and frames is not None:
             R.write_ppm(args.ppm, frames[0].cpu().numpy())
 
@@ -383,47 +454,87 @@ def pmc_traffic(kernel: str):
     return None, None
 
 
+def host_cpu():
+    """The host the CPU baseline ran on: logical CPUs, this process's CPU share, CPU model."""
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        share = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        share = os.cpu_count()
+    return {"nproc": os.cpu_count(), "affinity": share, "model": model or "unknown"}
+
+
 def cpu_baseline(obj, params, gpu_frame, layout, args, wl):
-    """Time the CPU restatement (oracle/, 'port') on every k-th 16x16 tile of the same frame with
-    --cpu-threads threads, and check the GPU's bytes on those tiles against it."""
+    """Time the CPU restatement (oracle/, 'port') on every k-th 16x16 tile of the same frame (C2:
+    the whole frame) with --cpu-threads threads, and on every --cpu-single-every-th of those tiles
+    with one thread; check the GPU's bytes on the sampled tiles against it."""
     import numpy as np
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     import oracle as O
     sc = O.OracleScene(obj)
     op = O.make_params(params.width, params.height, params.pf, params.max_lvl, lights=params.lights, flags=params.flags,
                        seed=params.seed)
-    tiles = list(range(0, layout.n_tiles, args.cpu_sample_every))
+    every = args.cpu_sample_every or wl.get("cpu_every", 96)
     threads = args.cpu_threads
-    rays = 0
-    max_d = 0
-    exact = 0
-    total = 0
-    t0 = time.perf_counter()
-    outs = []
-    for t in tiles:
-        ty, tx = divmod(t, layout.tiles_x)
-        x0, y0 = tx * layout.tile_w, ty * layout.tile_h
-        w = min(layout.tile_w, params.width - x0)
-        h = min(layout.tile_h, params.height - y0)
-        _, u8, c = sc.render(op, x0, y0, w, h, nthreads=threads)
-        rays += int(c.sum())
-        outs.append((x0, y0, w, h, u8))
-    dt = time.perf_counter() - t0
+
+    def rects(tiles):
+        for t in tiles:
+            ty, tx = divmod(t, layout.tiles_x)
+            x0, y0 = tx * layout.tile_w, ty * layout.tile_h
+            yield x0, y0, min(layout.tile_w, params.width - x0), min(layout.tile_h, params.height - y0)
+
+    def run(rs, nthreads):
+        rays, outs = 0, []
+        t0 = time.perf_counter()
+        for x0, y0, w, h in rs:
+            _, u8, c = sc.render(op, x0, y0, w, h, nthreads=nthreads)
+            rays += int(c.sum())
+            outs.append((x0, y0, w, h, u8))
+        return rays, time.perf_counter() - t0, outs
+
+    if every == 1:   # the whole frame in one call (row-interleaved threads)
+        rays, dt, outs = run([(0, 0, params.width, params.height)], threads)
+        what = f"the whole {params.width}x{params.height} frame"
+        tiles = list(range(0, layout.n_tiles, 97))
+    else:
+        tiles = list(range(0, layout.n_tiles, every))
+        rays, dt, outs = run(rects(tiles), threads)
+        what = f"{len(tiles)} of {layout.n_tiles} 16x16 tiles (every {every}th)"
+    # one thread: 4x4-pixel blocks at the sampled tiles' corners until the time budget is spent
+    rays1, dt1, blocks = 0, 0.0, 0
+    for x0, y0, w, h in rects(tiles):
+        r, d, _ = run([(x0, y0, min(w, 4), min(h, 4))], 1)
+        rays1, dt1, blocks = rays1 + r, dt1 + d, blocks + 1
+        if dt1 >= args.cpu_single_budget:
+            break
+    max_d = exact = total = 0
     for x0, y0, w, h, u8 in outs:
         g = gpu_frame[y0:y0 + h, x0:x0 + w]
         d = np.abs(g.astype(np.int16) - u8.astype(np.int16))
         max_d = max(max_d, int(d.max()))
         exact += int((d == 0).sum())
         total += d.size
-    import platform
+    hc = host_cpu()
     return {
         "value": round(rays / dt / 1e6, 6),
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{len(tiles)} of {layout.n_tiles} 16x16 tiles (every {args.cpu_sample_every}th) of the same "
-                  f"{wl['desc'].split(':')[0]} frame, {rays} rays in {dt:.1f} s, oracle/rt_oracle.c (-O2) on {threads} threads, "
-                  f"host {platform.processor() or platform.machine()}",
+        "sample": f"{what} of the same {wl['desc'].split(':')[0]} frame, {rays} rays in {dt:.1f} s, "
+                  f"oracle/rt_oracle.c (-O2, brute force) on {threads} threads",
+        "single_thread": {"value": round(rays1 / dt1 / 1e6, 6), "unit": "Mrays/s", "cores": 1,
+                          "sample": f"{blocks} 4x4-pixel blocks at sampled tiles, {rays1} rays in {dt1:.1f} s"},
+        "host": hc,
+        "host_note": f"{threads} threads = the GPU box's CPU share per GPU (nproc {hc['nproc']} counts the whole "
+                     f"machine's CPUs, most of them not ours)",
         "parity_vs_gpu": {"bytes": total, "exact_frac": round(exact / max(total, 1), 6), "max_lsb": max_d},
     }
 

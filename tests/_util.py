@@ -43,6 +43,8 @@ def scene_path(spec: str, workdir: str) -> str:
         materialize_models(workdir)
         return os.path.join(workdir, name)
     if kind == "syn":
+        if name == "balls":     # C3 surrogate (Balls.obj is missing from the reference)
+            return scenes.balls_surrogate(workdir)
         return scenes.write_sphere_grid(getattr(scenes, name), workdir, name.lower())
     raise ValueError(spec)
 

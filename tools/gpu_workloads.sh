@@ -1,10 +1,14 @@
 #!/bin/bash
-# Bench lines for the non-default BASELINE configs (no CPU baseline: C5's brute-force CPU cost is hours).
+# Bench lines for the non-default BASELINE configs. C2: the CPU baseline renders the whole frame;
+# C3: every 16th tile; C5: every 1024th tile, each with its in-run parity check.
+# C5 stochastic is parity-tested in tests/test_gpu_configs.py and runs without the CPU leg here.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-TAG=${1:-r01}
+TAG=${1:-r02}
 for W in c2 c3 c5 c5s; do
-  timeout -k 10 500 python bench.py --workload $W --no-cpu --no-bf-roofline > gpurun_out/bench_${TAG}_$W.json 2> gpurun_out/bench_${TAG}_$W.err || { echo "bench $W failed"; tail -20 gpurun_out/bench_${TAG}_$W.err; exit 1; }
-  python -c "import json,sys; d=json.load(open('gpurun_out/bench_${TAG}_$W.json')); print('$W', d['value'], 'Mrays/s', d['ms_per_step'], 'ms', d['config']['rays_per_step'], 'rays', 'load', d['config']['scene_load_s'], 'gen', d['config']['scene_gen_s'], d['kernel_ms_per_step'], d['accel'])"
+  EXTRA="--no-bf-roofline"
+  [ "$W" = "c5s" ] && EXTRA="$EXTRA --no-cpu"
+  timeout -k 10 900 python bench.py --workload $W $EXTRA > gpurun_out/bench_${TAG}_$W.json 2> gpurun_out/bench_${TAG}_$W.err || { echo "bench $W failed"; tail -20 gpurun_out/bench_${TAG}_$W.err; exit 1; }
+  python -c "import json,sys; d=json.load(open('gpurun_out/bench_${TAG}_$W.json')); c=d.get('cpu_baseline') or {}; print('$W', d['value'], 'Mrays/s', d['ms_per_step'], 'ms', 'cold', d['config']['first_frame_ms'], d['config']['rays_per_step'], 'rays', 'load', d['config']['scene_load_s'], 'cpu', c.get('value'), c.get('parity_vs_gpu'))"
 done
