@@ -175,3 +175,22 @@ def test_many_lights_full_frame(spec, w, h, pf, max_lvl, n_lights, workdir, gpu_
                                                nthreads=ORACLE_THREADS)
     assert [int(c) for c in counts] == [int(c) for c in oc]
     _close(u8, f32, ou8, of32)
+
+
+def test_oversized_sample_counts_are_rejected(workdir, gpu_available):
+    """A tile whose samples x lights exceed the int32 queue range, and pixel factors above 2^16
+    per pixel, are argument errors before anything is launched."""
+    import torch
+    from raytracert_amd import _capi
+    with R.Scene.load(scene_path("syn:F3", workdir), device=0) as sc:
+        buf = torch.zeros(64 * 64 * 3, dtype=torch.uint8, device="cuda:0")
+        lights = LIGHT_SETS[16]
+        p = R.RenderParams(width=64, height=64, pf=256, max_lvl=1, lights=lights)
+        with pytest.raises(R.RtError) as ei:   # 64*64*65536 samples x 16 lights > 2^30
+            sc.render_tiles_device(p, 64, 64, 0, 1, buf.data_ptr(), buf.numel())
+        assert ei.value.code == _capi.RT_E_ARG
+        with pytest.raises(R.RtError) as ei:
+            sc.render(R.RenderParams(width=8, height=8, pf=257, max_lvl=0), 0, 0, 1, 1)
+        assert ei.value.code == _capi.RT_E_ARG
+        u8, _, _ = sc.render(R.RenderParams(width=64, height=36, pf=2, max_lvl=1, lights=lights), 0, 0, 8, 8)
+        assert u8.shape == (8, 8, 3)   # the scene still renders afterwards
