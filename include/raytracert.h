@@ -10,6 +10,7 @@
  *   rt_scene_destroy      (globals live for the process: main.cpp:17-18,130)
  *   rt_scene_export       read access to MyMesh / normals   raytracing.h:8, raytracing.cpp:33
  *   rt_get_material       Material getMaterial(int)         raytracing.h:27, raytracing.cpp:373-376
+ *   rt_ray_intersect_triangle  rayIntersectTriangle (batched pairs)  raytracing.cpp:99-154
  *   rt_intersect_mesh     intersectMesh (batched)           raytracing.cpp:161-192
  *   rt_trace_rays         Vec3Df performRayTracing(o, d)    raytracing.h:33, raytracing.cpp:410-416
  *   rt_debug_trace        debug key 'd' (shoot + trace)     raytracing.cpp:493-510
@@ -120,12 +121,20 @@ int  rt_scene_create(const float *xyz, int32_t n_vertices, const uint32_t *tri_v
                      int32_t device, rt_scene **out);
 void rt_scene_destroy(rt_scene *scene);
 int  rt_scene_info(const rt_scene *scene, int32_t *n_vertices, int32_t *n_triangles, int32_t *n_materials);
-/* Host copies of the loaded scene; any pointer may be NULL. Sizes: 3*nv, 3*nt, nt, nm, 3*nt. */
+/* Host copies of the loaded scene; any pointer may be NULL. Sizes: 3*nv, 3*nt, nt, nm, 3*nt.
+ * face_normals of a device scene are the ones its renderer uses, computed on the device at upload
+ * (calculateNormals, raytracing.cpp:78-86); of a host-only scene, the loader's (bit-identical). */
 int  rt_scene_export(const rt_scene *scene, float *vertices, uint32_t *tri_v, uint32_t *tri_mat,
                      rt_material *materials, float *face_normals);
 int  rt_get_material(const rt_scene *scene, int32_t triangle_index, rt_material *out);
 
 /* ---- hot path ------------------------------------------------------------------------- */
+/* rayIntersectTriangle (raytracing.cpp:99-154) for n independent (ray, triangle) pairs on device
+ * `device`: rays = n x {origin, dest} (6 floats), tris = n x {T0, T1, T2} (9 floats), host arrays.
+ * hit[i] = 1 and points[3*i..] = the intersection point (the reference's intersectOut), or 0 and
+ * (0,0,0). No distance compare: a hit whose point is not finite is reported as the reference does. */
+int rt_ray_intersect_triangle(int32_t device, const float *rays, const float *tris, int32_t n, uint8_t *hit,
+                              float *points);
 /* Batched intersectMesh: n rays (origin[i], dest[i], host arrays of 3*n floats).
  * index_out[i] = closest triangle or -1; point_out[3*i..] = hit point or (0,0,0). */
 int rt_intersect_mesh(rt_scene *scene, const float *origins, const float *dests, int32_t n,

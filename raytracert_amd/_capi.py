@@ -86,6 +86,7 @@ _SIGNATURES = {
     "rt_scene_info": ([_VP, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)], C.c_int),
     "rt_scene_export": ([_VP, _VP, _VP, _VP, _VP, _VP], C.c_int),
     "rt_get_material": ([_VP, C.c_int32, C.POINTER(RtMaterial)], C.c_int),
+    "rt_ray_intersect_triangle": ([C.c_int32, _VP, _VP, C.c_int32, _VP, _VP], C.c_int),
     "rt_intersect_mesh": ([_VP, _VP, _VP, C.c_int32, _VP, _VP], C.c_int),
     "rt_trace_rays": ([_VP, C.POINTER(RtParams), _VP, _VP, C.c_int32, _VP, _VP], C.c_int),
     "rt_debug_trace": ([_VP, C.POINTER(RtParams), _VP, _VP, _VP, C.c_int32, C.POINTER(C.c_int32), _VP], C.c_int),

@@ -319,10 +319,24 @@ def bvh_acceptance_box(T) -> tuple[int, np.ndarray, np.ndarray]:
     return st, lo, hi
 
 
+def ray_intersect_triangle(rays, tris, device: int = 0):
+    """rayIntersectTriangle (raytracing.cpp:99-154) for n (ray, triangle) pairs on the GPU:
+    rays [n, 2, 3] (origin, dest), tris [n, 3, 3] -> (hit[n] bool, point[n, 3] float32)."""
+    R_ = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
+    T_ = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
+    if len(R_) != len(T_):
+        raise ValueError("rays and tris differ in length")
+    n = len(R_)
+    hit = np.zeros(n, np.uint8)
+    pts = np.zeros((n, 3), np.float32)
+    check(lib().rt_ray_intersect_triangle(device, _ptr(R_), _ptr(T_), n, _ptr(hit), _ptr(pts)))
+    return hit.astype(bool), pts
+
+
 def device_count() -> int:
     n = C.c_int32()
     check(lib().rt_device_count(C.byref(n)))
     return n.value
 
 
-__all__ = ["Scene", "RenderParams", "default_corners", "write_ppm", "device_count", "RT_HOST_ONLY"]
+__all__ = ["Scene", "RenderParams", "default_corners", "write_ppm", "device_count", "ray_intersect_triangle", "RT_HOST_ONLY"]

@@ -139,5 +139,9 @@ constexpr int kWaveBatch = 64;   // samples per wave batch of the chain launch (
 void launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream, bool xcd_segments = false);
 void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *dst, int32_t n,
                            int32_t *idx, float4 *I, hipStream_t stream);
+// calculateNormals on the device (face normal per triangle into normals[i].xyz)
+void launch_face_normals(const float *xyz, const uint32_t *tri_v, int32_t nt, float4 *normals, hipStream_t stream);
+// rayIntersectTriangle for n (ray, triangle) pairs: R = n x (origin, dest), T = n x 3 vertices
+void launch_ray_triangle_pairs(const float *R, const float *T, int32_t n, uint8_t *hit, float *I, hipStream_t stream);
 
 }  // namespace rt

@@ -1956,6 +1956,62 @@ __global__ __launch_bounds__(kOrderBlock) void k_order_scatter(const uint32_t *_
     }
 }
 
+// calculateNormals (raytracing.cpp:78-86) on the device, one lane per triangle:
+// normalize(crossProduct(v1 - v0, v2 - v0)) with Vec3D's operation order (Vec3D.h:142-151,185-191),
+// so each normal is bit-identical to the host loader's (scene_loader.cpp compute_face_normals).
+__global__ __launch_bounds__(kBlock) void k_face_normals(const float *__restrict__ xyz, const uint32_t *__restrict__ tri_v,
+                                                         int32_t nt, float4 *__restrict__ normals) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= nt) return;
+    const uint32_t ia = tri_v[3 * i], ib = tri_v[3 * i + 1], ic = tri_v[3 * i + 2];
+    const V3 p0 = mk(xyz[3 * ia], xyz[3 * ia + 1], xyz[3 * ia + 2]);
+    const V3 e01 = sub(mk(xyz[3 * ib], xyz[3 * ib + 1], xyz[3 * ib + 2]), p0);
+    const V3 e02 = sub(mk(xyz[3 * ic], xyz[3 * ic + 1], xyz[3 * ic + 2]), p0);
+    V3 n = mk(e01.y * e02.z - e01.z * e02.y, e01.z * e02.x - e01.x * e02.z, e01.x * e02.y - e01.y * e02.x);
+    normalize(n);
+    normals[i] = make_float4(n.x, n.y, n.z, 0.0f);
+}
+
+// rayIntersectTriangle (raytracing.cpp:99-154) for n independent (ray, triangle) pairs, every
+// step in the reference's order; unlike intersectMesh's use of it there is no distance compare, so
+// a hit whose point is NaN or infinite is still reported, as the reference returns true for it.
+// hit[i] = 1 and I[i] = the point, or 0 and (0,0,0).
+__global__ __launch_bounds__(kBlock) void k_ray_triangle_pairs(const float *__restrict__ R, const float *__restrict__ T,
+                                                               int32_t n, uint8_t *__restrict__ hit, float *__restrict__ I) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float *r = R + 6 * i, *t = T + 9 * i;
+    V3 out = mk(0, 0, 0);
+    uint8_t h = 0;
+    do {
+        const V3 T0 = mk(t[0], t[1], t[2]);
+        const V3 u = sub(mk(t[3], t[4], t[5]), T0), v = sub(mk(t[6], t[7], t[8]), T0);            // :106-107
+        const V3 nn = mk(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x);      // :108
+        if (nn.x == 0 && nn.y == 0 && nn.z == 0) break;                                             // :109
+        const V3 o = mk(r[0], r[1], r[2]);
+        const V3 dir = sub(mk(r[3], r[4], r[5]), o);                                                // :111
+        const V3 w0 = sub(o, T0);                                                                   // :112
+        const float b = dot(nn, dir);                                                               // :113
+        const float a = -dot(nn, w0);                                                               // :114
+        if (fabsf(b) < 0.00001f) break;                                                             // :115
+        const float rr = a / b;                                                                     // :124
+        if (rr < 0) break;                                                                          // :125
+        const V3 Ip = add(o, scale(dir, rr));                                                       // :130
+        const float uu = dot(u, u), uv = dot(u, v), vv = dot(v, v);                                 // :134-136
+        const V3 w = sub(Ip, T0);                                                                   // :137
+        const float wu = dot(w, u), wv = dot(w, v);                                                 // :138-139
+        const float D = uv * uv - uu * vv;                                                          // :140
+        const float ss = (uv * wv - vv * wu) / D;                                                   // :144
+        if (ss < 0 || ss > 1) break;
+        const float tt = (uv * wu - uu * wv) / D;                                                   // :148
+        if (tt < 0 || (ss + tt) > 1) break;
+        out = Ip;
+        h = 1;
+    } while (false);
+    hit[i] = h;
+    I[3 * i] = out.x; I[3 * i + 1] = out.y; I[3 * i + 2] = out.z;
+}
+
 inline unsigned grid_for(int64_t n) { return static_cast<unsigned>((n + kBlock - 1) / kBlock); }
 
 }  // namespace
@@ -2132,6 +2188,16 @@ void launch_intersect_only(const DevScene &s0, const float4 *org, const float4 *
         return;
     }
     hipLaunchKernelGGL(k_intersect_only, dim3(grid_for(n)), dim3(kBlock), 0, stream, s0.tris, s0.nt, org, dst, n, idx, I);
+}
+
+void launch_face_normals(const float *xyz, const uint32_t *tri_v, int32_t nt, float4 *normals, hipStream_t stream) {
+    if (nt <= 0) return;
+    hipLaunchKernelGGL(k_face_normals, dim3(grid_for(nt)), dim3(kBlock), 0, stream, xyz, tri_v, nt, normals);
+}
+
+void launch_ray_triangle_pairs(const float *R, const float *T, int32_t n, uint8_t *hit, float *I, hipStream_t stream) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_ray_triangle_pairs, dim3(grid_for(n)), dim3(kBlock), 0, stream, R, T, n, hit, I);
 }
 
 }  // namespace rt
