@@ -1,0 +1,425 @@
+/* raytracert_dropin.hpp — source-level drop-in for the reference tracer's headers over librtamd.so.
+ *
+ * The reference's render path is declared in CG_Project/raytracing.h (globals and functions), with
+ * its types in Vec3D.h, Vertex.h and mesh.h, and defined in raytracing.cpp + mesh.cpp. A host that
+ * replaces
+ *     #include "raytracing.h"          with          #include "raytracert_dropin.hpp"
+ * and drops raytracing.cpp and mesh.cpp from its build compiles its main.cpp unchanged: the frame
+ * loop of the 'r' key (main.cpp:340-411) keeps calling performRayTracing per sub-sample, and each
+ * call runs on the GPU. For speed the whole loop collapses into one call, renderImage(), whose
+ * clamped floats are exactly the loop's Image::_image (so writeImage produces the same PPM bytes).
+ *
+ *   reference                                   here
+ *   template Vec3D<T>, Vec3Df (Vec3D.h)         Vec3D<T> with the same operators and operation order
+ *   Vertex (Vertex.h), Triangle, Material,      the same members and accessors; Mesh::loadMesh
+ *   Mesh (mesh.h:10-201)                        loads through librtamd (mesh.cpp semantics)
+ *   globals of raytracing.h:8-16                declared extern here, defined by the host's main.cpp
+ *                                               as before (MyMesh, MyLightPositions, ...)
+ *   globals of raytracing.cpp:15-36             defined here (inline): Ambient..Refraction,
+ *                                               pixelfactorX/Y, max_lvl, normals
+ *   init, calculateNormals, getMaterial,        same signatures and meaning; the ray functions run
+ *   trace, performRayTracing, intersectMesh,    on the GPU scene built from MyMesh (uploadMesh())
+ *   rayIntersectTriangle, isNullVector
+ *
+ * Extra: RayTracerDevice (the GPU init() binds; RT_HOST_ONLY = loader only), uploadMesh() (re-upload
+ * MyMesh after editing it), renderImage() (the 'r' loop in one call), performRayTracing over
+ * vectors (batched). Failures throw rtamd_dropin::Error (the reference has no error path).
+ * Not provided (GL preview only, no effect on the image): Mesh::draw/drawSmooth, yourDebugDraw,
+ * the box/rectangle intersectors. Texture coordinates are not loaded (Mesh::texcoords stays
+ * empty, Triangle::t = 0): the render path never reads them. Header-only; C++17; link -lrtamd.
+ */
+#ifndef RAYTRACERT_DROPIN_HPP_
+#define RAYTRACERT_DROPIN_HPP_
+
+#include <cmath>
+#include <cstdint>
+#include <iostream>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "raytracert.h"
+
+// ---- Vec3D (Vec3D.h): component-wise operators; dot = (a0*b0 + a1*b1) + a2*b2 ----------------
+template <typename T>
+class Vec3D {
+  public:
+    T p[3];
+    Vec3D() { p[0] = p[1] = p[2] = T(); }
+    Vec3D(T x, T y, T z) { p[0] = x; p[1] = y; p[2] = z; }
+    Vec3D(const Vec3D &o) { p[0] = o.p[0]; p[1] = o.p[1]; p[2] = o.p[2]; }
+    explicit Vec3D(T *q) { p[0] = q[0]; p[1] = q[1]; p[2] = q[2]; }
+    T &operator[](int i) { return p[i]; }
+    const T &operator[](int i) const { return p[i]; }
+    Vec3D &operator=(const Vec3D &o) { p[0] = o.p[0]; p[1] = o.p[1]; p[2] = o.p[2]; return *this; }
+    Vec3D &operator+=(const Vec3D &o) { for (int k = 0; k < 3; ++k) p[k] += o.p[k]; return *this; }
+    Vec3D &operator-=(const Vec3D &o) { for (int k = 0; k < 3; ++k) p[k] -= o.p[k]; return *this; }
+    Vec3D &operator*=(const Vec3D &o) { for (int k = 0; k < 3; ++k) p[k] *= o.p[k]; return *this; }
+    Vec3D &operator*=(T s) { for (int k = 0; k < 3; ++k) p[k] *= s; return *this; }
+    Vec3D &operator/=(const Vec3D &o) { for (int k = 0; k < 3; ++k) p[k] /= o.p[k]; return *this; }
+    Vec3D &operator/=(T s) { for (int k = 0; k < 3; ++k) p[k] /= s; return *this; }
+    Vec3D &init(T x, T y, T z) { p[0] = x; p[1] = y; p[2] = z; return *this; }
+    T getSquaredLength() const { return dotProduct(*this, *this); }
+    T getLength() const { return static_cast<T>(std::sqrt(getSquaredLength())); }
+    // scales by the rounded reciprocal of the length (not a division per component)
+    T normalize() {
+        const T len = getLength();
+        if (len == 0.0f) return 0;
+        const T inv = 1.0f / len;
+        p[0] *= inv; p[1] *= inv; p[2] *= inv;
+        return len;
+    }
+    void fromTo(const Vec3D &a, const Vec3D &b) { for (int k = 0; k < 3; ++k) p[k] = b.p[k] - a.p[k]; }
+    float transProduct(const Vec3D &v) const { return p[0] * v[0] + p[1] * v[1] + p[2] * v[2]; }
+    Vec3D projectOn(const Vec3D &N, const Vec3D &P) const { return *this - N * dotProduct(*this - P, N); }
+    T *pointer() { return p; }
+    const T *pointer() const { return p; }
+    static Vec3D segment(const Vec3D &a, const Vec3D &b) { return Vec3D(b[0] - a[0], b[1] - a[1], b[2] - a[2]); }
+    static Vec3D crossProduct(const Vec3D &a, const Vec3D &b) {
+        return Vec3D(a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]);
+    }
+    static T dotProduct(const Vec3D &a, const Vec3D &b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+    static T squaredDistance(const Vec3D &a, const Vec3D &b) { return (a - b).getSquaredLength(); }
+    static T distance(const Vec3D &a, const Vec3D &b) { return (a - b).getLength(); }
+    static Vec3D interpolate(const Vec3D &u, const Vec3D &v, T alpha) { return u * (1.0f - alpha) + v * alpha; }
+    static Vec3D projectOntoVector(const Vec3D &v1, const Vec3D &v2) { return v2 * dotProduct(v1, v2); }
+};
+
+template <class T> const Vec3D<T> operator*(const Vec3D<T> &a, float f) { return Vec3D<T>(a[0] * f, a[1] * f, a[2] * f); }
+template <class T> const Vec3D<T> operator*(float f, const Vec3D<T> &a) { return Vec3D<T>(a[0] * f, a[1] * f, a[2] * f); }
+template <class T> const Vec3D<T> operator*(const Vec3D<T> &a, const Vec3D<T> &b) {
+    return Vec3D<T>(a[0] * b[0], a[1] * b[1], a[2] * b[2]);
+}
+template <class T> const Vec3D<T> operator+(const Vec3D<T> &a, const Vec3D<T> &b) {
+    return Vec3D<T>(a[0] + b[0], a[1] + b[1], a[2] + b[2]);
+}
+template <class T> const Vec3D<T> operator-(const Vec3D<T> &a, const Vec3D<T> &b) {
+    return Vec3D<T>(a[0] - b[0], a[1] - b[1], a[2] - b[2]);
+}
+template <class T> const Vec3D<T> operator-(const Vec3D<T> &a) { return Vec3D<T>(-a[0], -a[1], -a[2]); }
+template <class T> const Vec3D<T> operator/(const Vec3D<T> &a, float d) { return Vec3D<T>(a[0] / d, a[1] / d, a[2] / d); }
+template <class T> bool operator==(const Vec3D<T> &a, const Vec3D<T> &b) { return a[0] == b[0] && a[1] == b[1] && a[2] == b[2]; }
+template <class T> bool operator!=(const Vec3D<T> &a, const Vec3D<T> &b) { return !(a == b); }
+template <class T> bool operator<(const Vec3D<T> &a, const Vec3D<T> &b) { return a[0] < b[0] && a[1] < b[1] && a[2] < b[2]; }
+template <class T> bool operator>=(const Vec3D<T> &a, const Vec3D<T> &b) { return a[0] >= b[0] || a[1] >= b[1] || a[2] >= b[2]; }
+template <class T> std::ostream &operator<<(std::ostream &o, const Vec3D<T> &v) { return o << v[0] << " " << v[1] << " " << v[2]; }
+template <class T> std::istream &operator>>(std::istream &i, Vec3D<T> &v) { return i >> v[0] >> v[1] >> v[2]; }
+
+typedef Vec3D<float> Vec3Df;
+typedef Vec3D<double> Vec3Dd;
+typedef Vec3D<int> Vec3Di;
+static_assert(sizeof(Vec3Df) == sizeof(rt_vec3), "Vec3Df is three packed floats, as rt_vec3");
+
+// ---- Vertex, Triangle, Material, Mesh (Vertex.h, mesh.h) --------------------------------------
+class Vertex {
+  public:
+    Vertex() {}
+    Vertex(const Vec3Df &pos) : p(pos) {}
+    Vertex(const Vec3Df &pos, const Vec3Df &nrm) : p(pos), n(nrm) {}
+    Vec3Df p;   // position
+    Vec3Df n;   // vertex normal (Mesh::computeVertexNormals)
+};
+
+class Triangle {
+  public:
+    Triangle() { v[0] = v[1] = v[2] = 0; t[0] = t[1] = t[2] = 0; }
+    Triangle(unsigned v0, unsigned t0, unsigned v1, unsigned t1, unsigned v2, unsigned t2) {
+        v[0] = v0; v[1] = v1; v[2] = v2;
+        t[0] = t0; t[1] = t1; t[2] = t2;
+    }
+    unsigned int v[3];   // vertex indices
+    unsigned int t[3];   // texture-coordinate indices (not loaded here: 0)
+};
+
+class Material {
+  public:
+    Material() { cleanup(); }
+    void cleanup() { flags_ = 0; name_ = "empty"; }   // resets the flags only, as mesh.h:43-53
+    bool is_valid() const { return has(RT_HAS_KD) || has(RT_HAS_KA) || has(RT_HAS_KS) || has(RT_HAS_TR); }
+    bool has_Kd() const { return has(RT_HAS_KD); }
+    bool has_Ka() const { return has(RT_HAS_KA); }
+    bool has_Ks() const { return has(RT_HAS_KS); }
+    bool has_Ns() const { return has(RT_HAS_NS); }
+    bool has_Ni() const { return has(RT_HAS_NI); }
+    bool has_illum() const { return has(RT_HAS_ILLUM); }
+    bool has_Tr() const { return has(RT_HAS_TR); }
+    void set_Kd(float r, float g, float b) { Kd_ = Vec3Df(r, g, b); flags_ |= RT_HAS_KD; }
+    void set_Ka(float r, float g, float b) { Ka_ = Vec3Df(r, g, b); flags_ |= RT_HAS_KA; }
+    void set_Ks(float r, float g, float b) { Ks_ = Vec3Df(r, g, b); flags_ |= RT_HAS_KS; }
+    void set_Ns(float r) { Ns_ = r; flags_ |= RT_HAS_NS; }
+    void set_Ni(float r) { Ni_ = r; flags_ |= RT_HAS_NI; }
+    void set_illum(int r) { illum_ = r; flags_ |= RT_HAS_ILLUM; }
+    void set_Tr(float t) { Tr_ = t; flags_ |= RT_HAS_TR; }
+    void set_textureName(const std::string &s) { textureName_ = s; }
+    void set_name(const std::string &s) { name_ = s; }
+    const Vec3Df &Kd() const { return Kd_; }
+    const Vec3Df &Ka() const { return Ka_; }
+    const Vec3Df &Ks() const { return Ks_; }
+    float Ni() const { return Ni_; }
+    float Ns() const { return Ns_; }
+    int illum() const { return illum_; }
+    float Tr() const { return Tr_; }
+    const std::string &textureName() const { return textureName_; }
+    const std::string &name() const { return name_; }
+    // conversions to and from the C-ABI's plain material
+    static Material from_rt(const rt_material &m) {
+        Material o;
+        o.Kd_ = Vec3Df(m.Kd[0], m.Kd[1], m.Kd[2]);
+        o.Ka_ = Vec3Df(m.Ka[0], m.Ka[1], m.Ka[2]);
+        o.Ks_ = Vec3Df(m.Ks[0], m.Ks[1], m.Ks[2]);
+        o.Ns_ = m.Ns; o.Ni_ = m.Ni; o.Tr_ = m.Tr; o.illum_ = m.illum; o.flags_ = m.flags;
+        o.name_.clear();
+        return o;
+    }
+    rt_material to_rt() const {
+        rt_material m{};
+        for (int k = 0; k < 3; ++k) { m.Kd[k] = Kd_[k]; m.Ka[k] = Ka_[k]; m.Ks[k] = Ks_[k]; }
+        m.Ns = Ns_; m.Ni = Ni_; m.Tr = Tr_; m.illum = illum_; m.flags = flags_;
+        return m;
+    }
+
+  private:
+    bool has(uint32_t f) const { return (flags_ & f) != 0; }
+    // never-set values read 0 (the reference reads uninitialised memory there)
+    Vec3Df Kd_, Ka_, Ks_;
+    float Ns_ = 0, Ni_ = 0, Tr_ = 0;
+    int illum_ = 0;
+    uint32_t flags_ = 0;
+    std::string name_, textureName_;
+};
+
+namespace rtamd_dropin {
+class Error : public std::runtime_error {
+  public:
+    Error(int code, const std::string &what) : std::runtime_error(what), code_(code) {}
+    int code() const { return code_; }
+
+  private:
+    int code_;
+};
+inline void check(int rc) {
+    if (rc != RT_OK) throw Error(rc, rt_last_error_string());
+}
+}  // namespace rtamd_dropin
+
+class Mesh {
+  public:
+    Mesh() {}
+    Mesh(const std::vector<Vertex> &v, const std::vector<Triangle> &t) : vertices(v), triangles(t) {}
+    // Mesh::loadMesh (mesh.cpp:95-331, with loadMtl :334-460): through librtamd's loader, which
+    // keeps the reference's parse semantics; false when the file cannot be read (the reference
+    // crashes there, mesh.cpp:329)
+    bool loadMesh(const char *filename, bool /*randomizeTriangulation: disabled in the reference too*/) {
+        rt_scene *s = nullptr;
+        if (rt_scene_load_obj(filename, RT_HOST_ONLY, &s) != RT_OK) return false;
+        int32_t nv = 0, nt = 0, nm = 0;
+        rt_scene_info(s, &nv, &nt, &nm);
+        std::vector<float> xyz(3 * static_cast<size_t>(nv));
+        std::vector<uint32_t> tv(3 * static_cast<size_t>(nt));
+        std::vector<rt_material> mats(static_cast<size_t>(nm));
+        triangleMaterials.assign(static_cast<size_t>(nt), 0u);
+        rt_scene_export(s, xyz.data(), tv.data(), triangleMaterials.data(), mats.data(), nullptr);
+        rt_scene_destroy(s);
+        vertices.assign(static_cast<size_t>(nv), Vertex());
+        for (int32_t i = 0; i < nv; ++i) vertices[i].p = Vec3Df(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]);
+        triangles.assign(static_cast<size_t>(nt), Triangle());
+        for (int32_t i = 0; i < nt; ++i)
+            for (int k = 0; k < 3; ++k) triangles[i].v[k] = tv[3 * i + k];
+        materials.clear();
+        for (const rt_material &m : mats) materials.push_back(Material::from_rt(m));
+        texcoords.clear();
+        return true;
+    }
+    // Mesh::computeVertexNormals (mesh.cpp:28-47): the sum of the adjacent face normals, normalised
+    // (the GL preview's smooth shading; the render path does not read it)
+    void computeVertexNormals() {
+        for (Vertex &v : vertices) v.n = Vec3Df(0, 0, 0);
+        for (const Triangle &t : triangles) {
+            Vec3Df n = Vec3Df::crossProduct(vertices[t.v[1]].p - vertices[t.v[0]].p, vertices[t.v[2]].p - vertices[t.v[0]].p);
+            n.normalize();
+            for (int j = 0; j < 3; ++j) vertices[t.v[j]].n += n;
+        }
+        for (Vertex &v : vertices) v.n.normalize();
+    }
+    std::vector<Vertex> vertices;
+    std::vector<Vec3Df> texcoords;
+    std::vector<Triangle> triangles;
+    std::vector<unsigned int> triangleMaterials;
+    std::vector<Material> materials;
+};
+
+// ---- globals ------------------------------------------------------------------------------------
+// raytracing.h:8-16 — defined by the host (main.cpp:17-18,130,137-141), as with the reference
+extern Mesh MyMesh;
+extern std::vector<Vec3Df> MyLightPositions;
+extern Vec3Df MyCameraPosition;
+extern unsigned int WindowSize_X;
+extern unsigned int WindowSize_Y;
+extern unsigned int RayTracingResolutionX;
+extern unsigned int RayTracingResolutionY;
+// raytracing.cpp:15-36 — defined here (the reference defines them in raytracing.cpp)
+inline bool Ambient = true;
+inline bool Diffuse = true;
+inline bool Reflection = true;
+inline bool Shadows = true;
+inline bool Specular = true;
+inline bool Refraction = true;
+inline bool WireFrame = false;
+inline unsigned int pixelfactorX = 3;
+inline unsigned int pixelfactorY = 3;
+inline int max_lvl = 10;
+inline std::vector<Vec3Df> normals;   // per-triangle normals (calculateNormals)
+// the GPU init() binds (a HIP device index), or RT_HOST_ONLY: loader and getMaterial only
+inline int RayTracerDevice = 0;
+
+namespace rtamd_dropin {
+inline rt_scene *&scene() {
+    static rt_scene *s = nullptr;
+    return s;
+}
+inline rt_scene *need_scene() {
+    if (!scene()) throw Error(RT_E_ARG, "no GPU scene: call init() (with RayTracerDevice a device index) first");
+    return scene();
+}
+// Everything the reference reads from globals during a trace.
+inline rt_params params(int levels_left) {
+    if (MyLightPositions.size() > RT_MAX_LIGHTS) throw Error(RT_E_ARG, "at most 16 lights");
+    rt_params p{};
+    p.width = static_cast<int32_t>(WindowSize_X);
+    p.height = static_cast<int32_t>(WindowSize_Y);
+    p.pfx = static_cast<int32_t>(pixelfactorX);
+    p.pfy = static_cast<int32_t>(pixelfactorY);
+    p.max_lvl = levels_left;
+    p.flags = (Ambient ? RT_AMBIENT : 0u) | (Diffuse ? RT_DIFFUSE : 0u) | (Specular ? RT_SPECULAR : 0u) |
+              (Reflection ? RT_REFLECTION : 0u) | (Shadows ? RT_SHADOWS : 0u) | (Refraction ? RT_REFRACTION : 0u);
+    p.n_lights = static_cast<int32_t>(MyLightPositions.size());
+    for (size_t i = 0; i < MyLightPositions.size(); ++i)
+        for (int k = 0; k < 3; ++k) p.lights[i][k] = MyLightPositions[i][k];
+    for (int k = 0; k < 3; ++k) p.camera_pos[k] = MyCameraPosition[k];
+    p.seed = RT_DEFAULT_SEED;
+    return p;
+}
+}  // namespace rtamd_dropin
+
+// (Re)build the GPU scene from MyMesh: call after editing MyMesh by hand. init() calls it.
+inline void uploadMesh() {
+    rt_scene_destroy(rtamd_dropin::scene());
+    rtamd_dropin::scene() = nullptr;
+    if (RayTracerDevice == RT_HOST_ONLY) return;
+    std::vector<float> xyz;
+    xyz.reserve(3 * MyMesh.vertices.size());
+    for (const Vertex &v : MyMesh.vertices) { xyz.push_back(v.p[0]); xyz.push_back(v.p[1]); xyz.push_back(v.p[2]); }
+    std::vector<uint32_t> tv;
+    tv.reserve(3 * MyMesh.triangles.size());
+    for (const Triangle &t : MyMesh.triangles) { tv.push_back(t.v[0]); tv.push_back(t.v[1]); tv.push_back(t.v[2]); }
+    std::vector<rt_material> mats;
+    for (const Material &m : MyMesh.materials) mats.push_back(m.to_rt());
+    rtamd_dropin::check(rt_scene_create(xyz.data(), static_cast<int32_t>(MyMesh.vertices.size()), tv.data(),
+                                        MyMesh.triangleMaterials.data(), static_cast<int32_t>(MyMesh.triangles.size()),
+                                        mats.data(), static_cast<int32_t>(mats.size()), RayTracerDevice,
+                                        &rtamd_dropin::scene()));
+}
+
+// calculateNormals (raytracing.cpp:78-86): one normal per triangle into `normals` (appended, as
+// the reference's push_back); on a GPU scene these are the device-computed normals it renders with
+inline void calculateNormals() {
+    const size_t nt = MyMesh.triangles.size();
+    std::vector<float> n(3 * nt);
+    rt_scene *s = rtamd_dropin::scene();
+    bool own = false;
+    if (!s) {   // host only: the loader's normals of MyMesh
+        std::vector<float> xyz;
+        for (const Vertex &v : MyMesh.vertices) { xyz.push_back(v.p[0]); xyz.push_back(v.p[1]); xyz.push_back(v.p[2]); }
+        std::vector<uint32_t> tv;
+        for (const Triangle &t : MyMesh.triangles) { tv.push_back(t.v[0]); tv.push_back(t.v[1]); tv.push_back(t.v[2]); }
+        std::vector<rt_material> mats(1);
+        mats[0].flags = RT_HAS_KD;
+        std::vector<uint32_t> tm(nt, 0u);
+        rtamd_dropin::check(rt_scene_create(xyz.data(), static_cast<int32_t>(MyMesh.vertices.size()), tv.data(), tm.data(),
+                                            static_cast<int32_t>(nt), mats.data(), 1, RT_HOST_ONLY, &s));
+        own = true;
+    }
+    const int rc = rt_scene_export(s, nullptr, nullptr, nullptr, nullptr, n.data());
+    if (own) rt_scene_destroy(s);
+    rtamd_dropin::check(rc);
+    for (size_t i = 0; i < nt; ++i) normals.push_back(Vec3Df(n[3 * i], n[3 * i + 1], n[3 * i + 2]));
+}
+
+// init(char*), raytracing.cpp:42-73
+inline void init(char *fileName) {
+    const char *path = fileName ? fileName : "cube.obj";
+    if (!MyMesh.loadMesh(path, true)) throw rtamd_dropin::Error(RT_E_IO, std::string("cannot load '") + path + "'");
+    MyMesh.computeVertexNormals();
+    uploadMesh();
+    calculateNormals();
+    MyLightPositions.push_back(MyCameraPosition);   // light 0 = the camera position (:72)
+}
+
+// isNullVector (raytracing.cpp:92-94)
+inline bool isNullVector(Vec3Df v) { return v[0] == 0 && v[1] == 0 && v[2] == 0; }
+
+// rayIntersectTriangle (raytracing.cpp:99-154), on the GPU bound by RayTracerDevice
+inline bool rayIntersectTriangle(Vec3Df R[], Vec3Df T[], Vec3Df *intersectOut) {
+    float r[6] = {R[0][0], R[0][1], R[0][2], R[1][0], R[1][1], R[1][2]};
+    float t[9];
+    for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k) t[3 * i + k] = T[i][k];
+    uint8_t hit = 0;
+    float I[3];
+    rtamd_dropin::check(rt_ray_intersect_triangle(RayTracerDevice, r, t, 1, &hit, I));
+    if (hit && intersectOut) *intersectOut = Vec3Df(I[0], I[1], I[2]);
+    return hit != 0;
+}
+
+// intersectMesh (raytracing.cpp:161-192): closest triangle or -1; the point, or (0,0,0)
+inline int intersectMesh(Vec3Df origin, Vec3Df dest, Vec3Df *intersectOut) {
+    int32_t idx = -1;
+    float I[3] = {0, 0, 0};
+    rtamd_dropin::check(rt_intersect_mesh(rtamd_dropin::need_scene(), origin.p, dest.p, 1, &idx, I));
+    if (intersectOut) *intersectOut = Vec3Df(I[0], I[1], I[2]);
+    return idx;
+}
+
+// getMaterial (raytracing.cpp:373-376)
+inline Material getMaterial(int index) { return MyMesh.materials[MyMesh.triangleMaterials[index]]; }
+
+// trace (raytracing.cpp:381-406): every level test is `lvl < max_lvl` with unit steps, so trace
+// at lvl is the chain with max_lvl - lvl levels left
+inline Vec3Df trace(const Vec3Df &origin, const Vec3Df &dest, int lvl) {
+    const rt_params p = rtamd_dropin::params(lvl >= max_lvl ? 0 : max_lvl - lvl);
+    Vec3Df c;
+    rtamd_dropin::check(rt_trace_rays(rtamd_dropin::need_scene(), &p, origin.p, dest.p, 1, c.p, nullptr));
+    return c;
+}
+
+// performRayTracing (raytracing.cpp:410-416)
+inline Vec3Df performRayTracing(const Vec3Df &origin, const Vec3Df &dest) { return trace(origin, dest, 0); }
+
+// the same for many rays in one GPU call
+inline std::vector<Vec3Df> performRayTracing(const std::vector<Vec3Df> &origins, const std::vector<Vec3Df> &dests) {
+    if (origins.size() != dests.size()) throw rtamd_dropin::Error(RT_E_ARG, "origins/dests size mismatch");
+    std::vector<Vec3Df> out(origins.size());
+    if (origins.empty()) return out;
+    const rt_params p = rtamd_dropin::params(max_lvl);
+    rtamd_dropin::check(rt_trace_rays(rtamd_dropin::need_scene(), &p, origins[0].p, dests[0].p,
+                                      static_cast<int32_t>(origins.size()), out[0].p, nullptr));
+    return out;
+}
+
+// The 'r' key's loop (main.cpp:355-395) in one call: for the four corner rays produceRay gives,
+// the clamped RGB floats of every pixel, row-major from the top row, i.e. Image::_image after
+// the loop's setPixel(x, y, RGBValue(rgb)) calls. rays (may be NULL): queries per kind.
+inline std::vector<float> renderImage(const Vec3Df &origin00, const Vec3Df &dest00, const Vec3Df &origin01,
+                                      const Vec3Df &dest01, const Vec3Df &origin10, const Vec3Df &dest10,
+                                      const Vec3Df &origin11, const Vec3Df &dest11, uint64_t rays[3] = nullptr) {
+    rt_params p = rtamd_dropin::params(max_lvl);
+    const Vec3Df *c[8] = {&origin00, &dest00, &origin01, &dest01, &origin10, &dest10, &origin11, &dest11};
+    for (int i = 0; i < 8; ++i)
+        for (int k = 0; k < 3; ++k) p.corners[i][k] = (*c[i])[k];
+    std::vector<float> img(3u * WindowSize_X * WindowSize_Y);
+    rtamd_dropin::check(rt_render_tile(rtamd_dropin::need_scene(), &p, 0, 0, p.width, p.height, nullptr, img.data(), rays));
+    return img;
+}
+
+#endif  // RAYTRACERT_DROPIN_HPP_
