@@ -87,6 +87,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16, help="the GPU box's CPU share (16 per GPU)")
     ap.add_argument("--cpu-single-budget", type=float, default=15.0,
                     help="1-thread CPU figure: seconds spent on 4x4-pixel blocks of the sampled tiles")
+    ap.add_argument("--comm", choices=("torch", "rt"), default="torch",
+                    help="N>1 gather: torch.distributed (RCCL) + the library's un-permute kernel, or the library's own "
+                         "RCCL communicator end to end (rt_render_frames_sharded)")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold (unordered) first-frame measurement")
     ap.add_argument("--no-path-compare", action="store_true",
                     help="N=1: skip timing the shard path (tiles + un-permute) beside the frame path")
@@ -149,6 +152,14 @@ def main():
 
     layout = rdist.TileLayout(WIDTH, HEIGHT, TILE, TILE)
     stream = torch.cuda.current_stream(dev)
+    rtcomm = None
+    if args.comm == "rt":   # the library's communicator: rank 0's id broadcast over torch.distributed
+        uid = torch.zeros(R._capi.COMM_ID_BYTES, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(R.Comm.unique_id()), dtype=torch.uint8))
+        if world > 1:
+            dist.broadcast(uid, 0)
+        rtcomm = R.Comm(local_rank, rank, world, bytes(uid.cpu().numpy().tobytes()))
 
     class Runner:
         """One way of rendering a step. frames: frames per step (weak: N, strong: 1); frame_path:
@@ -164,6 +175,11 @@ def main():
             self.index = torch.as_tensor(self.plan.gather_index(), device=dev)
             if frame_path:
                 self.fbufs = [torch.zeros(HEIGHT * WIDTH * 3, dtype=torch.uint8, device=dev) for _ in range(2)]
+            elif rank == 0:
+                self.frames_out = [torch.zeros(frames * HEIGHT * WIDTH * 3, dtype=torch.uint8, device=dev) for _ in range(2)]
+            else:
+                self.frames_out = [torch.zeros(1, dtype=torch.uint8, device=dev)] * 2
+            self.nfin = 0
             self.pending = []
 
         def render_shard(self, want_counts=False, buf=None):
@@ -183,17 +199,28 @@ def main():
             return self.render_shard(buf=self.bufs[i % 2])
 
         def finish(self, p):
-            # order the stream after the gather, then un-permute on rank 0
+            # order the stream after the gather, then un-permute on rank 0 (the library's kernel)
             gathered, work = p
             if work is not None:
                 work.wait()
-            return rdist.assemble_plan_torch(gathered, self.plan, self.index) if rank == 0 else None
+            if rank != 0:
+                return None
+            out = self.frames_out[self.nfin % 2]
+            self.nfin += 1
+            R.assemble_tiles_device(local_rank, WIDTH, HEIGHT, TILE, TILE, self.plan.frames, world, gathered.data_ptr(),
+                                    gathered.numel(), out.data_ptr(), out.numel(), stream.cuda_stream)
+            return out.view(self.plan.frames, HEIGHT, WIDTH, 3)
 
         def step(self, i):
             """Render step i, start its gather (async, on the collective's stream) and finish step
             i-1's: the gather of one step overlaps the next step's render."""
             if self.single:
                 return self.render_once(i).view(1, HEIGHT, WIDTH, 3)
+            if rtcomm is not None:   # render + RCCL gather + un-permute, all inside the library
+                out = self.frames_out[i % 2]
+                scene.render_frames_sharded(cparams, rtcomm, TILE, TILE, self.plan.frames, out.data_ptr() if rank == 0 else None,
+                                            out.numel() if rank == 0 else 0, stream.cuda_stream)
+                return out.view(self.plan.frames, HEIGHT, WIDTH, 3) if rank == 0 else None
             self.render_shard(buf=self.bufs[i % 2])
             self.pending.append(rdist.gather_shards(self.bufs[i % 2], rank, world, async_op=True))
             return self.finish(self.pending.pop(0)) if len(self.pending) > 1 else None
@@ -226,7 +253,7 @@ def main():
                 dist.all_reduce(el, op=dist.ReduceOp.MAX)
             return float(el.item()), frames
 
-    main_run = Runner(world if args.mode == "weak" else 1, frame_path=world == 1)
+    main_run = Runner(world if args.mode == "weak" else 1, frame_path=world == 1 and rtcomm is None)
     plan = main_run.plan
 
     # rays per step (deterministic): counted once, summed over ranks
@@ -376,7 +403,9 @@ def main():
                 "width": WIDTH, "height": HEIGHT, "pf": PF, "max_lvl": MAX_LVL, "lights": [list(l) for l in LIGHTS],
                 "triangles": nt, "vertices": nv, "tile": TILE,
                 "parallelism": f"tile-shard{world}",
-                "path": "rt_render_frame_device" if main_run.single else "rt_render_tiles_device + RCCL gather + un-permute",
+                "path": ("rt_render_frame_device" if main_run.single else
+                         "rt_render_frames_sharded (library RCCL gather + un-permute)" if rtcomm is not None else
+                         "rt_render_tiles_device + RCCL gather (torch.distributed) + rt_assemble_tiles_device"),
                 "rays_per_step": int(rays_per_step),
                 "rays_by_kind_per_step": {"primary": rays_by_kind[0], "secondary": rays_by_kind[1], "shadow": rays_by_kind[2]},
                 "frame_ms_per_gpu": round(elapsed / args.steps * 1e3, 3),
@@ -428,6 +457,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(obj, params, frames[0].cpu().numpy(), layout, args, wl)
 
+    if rtcomm is not None:
+        rtcomm.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -19,6 +19,8 @@
  *                         + RGBValue clamp :24-42 + Image::writeImage quantisation :102-128)
  *   rt_render_tiles_device  same loop, interleaved tile shard into a device buffer (multi-GPU)
  *   rt_render_frame_device  same loop, the whole frame into a device buffer (single GPU)
+ *   rt_render_frames_sharded  the same loop over N GPUs     (nothing in the reference: SURVEY.md §8e)
+ *   rt_comm_*             RCCL communicator for it          (one process or host thread per GPU)
  *   rt_default_corners    produceRay for the 4 corners      main.cpp:300-325,355-358 (+ reshape :288-296)
  *   rt_write_ppm          Image::writeImage                 main.cpp:102-128
  *
@@ -43,6 +45,7 @@ extern "C" {
 #define RT_E_ARG    -4   /* invalid argument (NULL, negative size, bad tile, too many lights) */
 #define RT_E_NOMEM  -5
 #define RT_E_NODEV  -6   /* no usable gfx950 device */
+#define RT_E_RCCL   -7   /* an RCCL call failed, or the communicator reported an asynchronous error */
 
 #define RT_MAX_LIGHTS 16
 
@@ -181,6 +184,36 @@ int rt_render_frame_device(rt_scene *scene, const rt_params *params, int32_t til
 int rt_render_tiles_device(rt_scene *scene, const rt_params *params, int32_t tile_w, int32_t tile_h,
                            int32_t frames, int32_t first, int32_t stride, void *d_out_u8, size_t out_capacity,
                            void *stream, int32_t *n_tiles_out, uint64_t counts[3]);
+
+/* ---- multi-GPU ---------------------------------------------------------- */
+/* One rank per GPU (a process or a host thread each). Rank 0 makes an id with rt_comm_unique_id
+ * and the host hands its RT_COMM_ID_BYTES bytes to every rank (file, MPI, a TCP store...); every
+ * rank then calls rt_comm_init (collective: it returns when all nranks have joined). RCCL
+ * (librccl.so.1) is loaded on first use. */
+#define RT_COMM_ID_BYTES 128
+typedef struct rt_comm rt_comm;
+int  rt_comm_unique_id(uint8_t id[RT_COMM_ID_BYTES]);
+int  rt_comm_init(int32_t device, int32_t rank, int32_t nranks, const uint8_t id[RT_COMM_ID_BYTES], rt_comm **out);
+void rt_comm_destroy(rt_comm *comm);
+int  rt_comm_info(const rt_comm *comm, int32_t *rank, int32_t *nranks, int32_t *device);
+/* Polls the communicator (ncclCommGetAsyncError): RT_OK or RT_E_RCCL with the error's text. */
+int  rt_comm_check(rt_comm *comm);
+/* The 'r' loop over the communicator's GPUs. Collective: every rank calls it with the same params,
+ * tiling and frame count, its scene on its own device. `frames` frames of the view are cut into
+ * tile_w x tile_h tiles, ids g = f*T + t; rank r renders ids r, r+N, ... (rt_render_tiles_device),
+ * ONE gather (RCCL, equal-sized shards) brings the quantised tiles to rank 0, which un-permutes them
+ * on the device into d_frames_out: frames x height x width x 3 bytes, row-major, the PPM's order
+ * (other ranks: d_frames_out may be NULL). Bytes equal the one-GPU render's. Asynchronous on the
+ * caller's `stream` unless counts != NULL (this rank's queries per kind; then it synchronises and
+ * polls the communicator). */
+int rt_render_frames_sharded(rt_scene *scene, const rt_params *params, rt_comm *comm, int32_t tile_w, int32_t tile_h,
+                             int32_t frames, void *d_frames_out, size_t out_capacity, void *stream, uint64_t counts[3]);
+/* The un-permute step alone: d_gathered = nranks shards of slots = ceil(frames*T / nranks) tiles
+ * each (tile g in shard g % nranks, slot g / nranks; tile_w*tile_h*3 bytes per tile, row-major
+ * inside the tile) -> d_frames_out as above. For hosts that gather with their own transport. */
+int rt_assemble_tiles_device(int32_t device, int32_t width, int32_t height, int32_t tile_w, int32_t tile_h, int32_t frames,
+                             int32_t nranks, const void *d_gathered, size_t gathered_bytes, void *d_frames_out,
+                             size_t out_capacity, void *stream);
 
 /* ---- helpers -------------------------------------------------------------------------- */
 /* Corner rays of the reference's default view (camera at (0,0,4), fovy 50, near 1, far 10). */

@@ -7,7 +7,8 @@ package is a thin Python mirror of that interface for tests, the benchmark and m
 orchestration (torch.distributed over RCCL).
 """
 from ._capi import ALL_FEATURES, RtError, RT_HOST_ONLY  # noqa: F401
-from .api import RenderParams, Scene, default_corners, device_count, ray_intersect_triangle, write_ppm  # noqa: F401
+from .api import (Comm, RenderParams, Scene, assemble_tiles_device, default_corners, device_count,  # noqa: F401
+                  ray_intersect_triangle, write_ppm)
 
-__all__ = ["Scene", "RenderParams", "default_corners", "write_ppm", "device_count", "ray_intersect_triangle", "RtError",
+__all__ = ["Scene", "RenderParams", "Comm", "assemble_tiles_device", "default_corners", "write_ppm", "device_count", "ray_intersect_triangle", "RtError",
            "ALL_FEATURES", "RT_HOST_ONLY"]

@@ -21,6 +21,8 @@ RT_E_HIP = -3
 RT_E_ARG = -4
 RT_E_NOMEM = -5
 RT_E_NODEV = -6
+RT_E_RCCL = -7
+COMM_ID_BYTES = 128
 RT_HOST_ONLY = -1
 RT_MAX_LIGHTS = 16
 
@@ -109,6 +111,15 @@ _SIGNATURES = {
     "rt_scene_bvh_validate": ([_VP], C.c_int),
     "rt_bvh_acceptance_box": ([_VP, _VP, _VP], C.c_int),
     "rt_scene_tune": ([_VP, C.c_int32, C.c_int32], C.c_int),
+    "rt_comm_unique_id": ([_VP], C.c_int),
+    "rt_comm_init": ([C.c_int32, C.c_int32, C.c_int32, _VP, C.POINTER(_VP)], C.c_int),
+    "rt_comm_destroy": ([_VP], None),
+    "rt_comm_info": ([_VP, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)], C.c_int),
+    "rt_comm_check": ([_VP], C.c_int),
+    "rt_render_frames_sharded": ([_VP, C.POINTER(RtParams), _VP, C.c_int32, C.c_int32, C.c_int32, _VP, C.c_size_t, _VP,
+                                  _VP], C.c_int),
+    "rt_assemble_tiles_device": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP,
+                                  C.c_size_t, _VP, C.c_size_t, _VP], C.c_int),
 }
 
 _lib = None

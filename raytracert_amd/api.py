@@ -227,6 +227,18 @@ class Scene:
                                            C.c_void_p(stream_ptr) if stream_ptr else None, _ptr(counts)))
         return counts
 
+    def render_frames_sharded(self, params: RenderParams | RtParams, comm: "Comm", tile_w: int, tile_h: int, frames: int,
+                              out_ptr: int | None, out_capacity: int, stream_ptr: int | None = None,
+                              want_counts: bool = False):
+        """rt_render_frames_sharded: this rank's interleaved tiles, one RCCL gather to rank 0 and the
+        device un-permute there into out_ptr (frames x H x W x 3 bytes; rank 0 only)."""
+        p = params.to_c() if isinstance(params, RenderParams) else params
+        counts = np.zeros(3, np.uint64) if want_counts else None
+        check(lib().rt_render_frames_sharded(self._h, C.byref(p), comm.handle, tile_w, tile_h, frames,
+                                             C.c_void_p(out_ptr) if out_ptr else None, out_capacity,
+                                             C.c_void_p(stream_ptr) if stream_ptr else None, _ptr(counts)))
+        return counts
+
     # -- acceleration ------------------------------------------------------------------------
     def set_accel(self, mode) -> None:
         """'bvh' / 'brute_force' (or RT_ACCEL_* ints). Results are identical either way."""
@@ -319,6 +331,57 @@ def bvh_acceptance_box(T) -> tuple[int, np.ndarray, np.ndarray]:
     return st, lo, hi
 
 
+class Comm:
+    """An RCCL communicator of the library (rt_comm_*): one rank per GPU. Rank 0 calls
+    Comm.unique_id() and hands the bytes to every rank, which then constructs Comm(...)."""
+
+    def __init__(self, device: int, rank: int, nranks: int, uid: bytes):
+        if len(uid) != _capi.COMM_ID_BYTES:
+            raise ValueError("communicator id must be 128 bytes")
+        buf = (C.c_uint8 * _capi.COMM_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        check(lib().rt_comm_init(device, rank, nranks, buf, C.byref(h)))
+        self._h = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * _capi.COMM_ID_BYTES)()
+        check(lib().rt_comm_unique_id(buf))
+        return bytes(buf)
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    def info(self) -> tuple[int, int, int]:
+        r, n, d = C.c_int32(), C.c_int32(), C.c_int32()
+        check(lib().rt_comm_info(self._h, C.byref(r), C.byref(n), C.byref(d)))
+        return r.value, n.value, d.value
+
+    def check(self) -> None:
+        check(lib().rt_comm_check(self._h))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().rt_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def assemble_tiles_device(device: int, width: int, height: int, tile_w: int, tile_h: int, frames: int, nranks: int,
+                          gathered_ptr: int, gathered_bytes: int, out_ptr: int, out_capacity: int,
+                          stream_ptr: int | None = None) -> None:
+    """rt_assemble_tiles_device: un-permute gathered tile shards into frames x H x W x 3 bytes."""
+    check(lib().rt_assemble_tiles_device(device, width, height, tile_w, tile_h, frames, nranks, C.c_void_p(gathered_ptr),
+                                         gathered_bytes, C.c_void_p(out_ptr), out_capacity,
+                                         C.c_void_p(stream_ptr) if stream_ptr else None))
+
+
 def ray_intersect_triangle(rays, tris, device: int = 0):
     """rayIntersectTriangle (raytracing.cpp:99-154) for n (ray, triangle) pairs on the GPU:
     rays [n, 2, 3] (origin, dest), tris [n, 3, 3] -> (hit[n] bool, point[n, 3] float32)."""
@@ -339,4 +402,5 @@ def device_count() -> int:
     return n.value
 
 
-__all__ = ["Scene", "RenderParams", "default_corners", "write_ppm", "device_count", "ray_intersect_triangle", "RT_HOST_ONLY"]
+__all__ = ["Scene", "RenderParams", "Comm", "default_corners", "write_ppm", "device_count", "ray_intersect_triangle",
+           "assemble_tiles_device", "RT_HOST_ONLY"]

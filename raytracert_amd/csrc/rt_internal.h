@@ -136,4 +136,9 @@ void build_dev_materials(const HostScene &s, std::vector<DevMaterial> &out);
 // table (|x| < 2, sorted bit patterns of |x|); on each of them glibc returns the next float up.
 const uint32_t *powf2_tie_table(size_t *n);
 
+// Error slot of the C-ABI (rt_last_error_string) for the library's other translation units, and
+// the device a scene is bound to (RT_HOST_ONLY for host-only scenes).
+int set_error(int code, const std::string &msg);
+int scene_device(const rt_scene *s);
+
 }  // namespace rt

@@ -141,6 +141,10 @@ void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *d
                            int32_t *idx, float4 *I, hipStream_t stream);
 // calculateNormals on the device (face normal per triangle into normals[i].xyz)
 void launch_face_normals(const float *xyz, const uint32_t *tri_v, int32_t nt, float4 *normals, hipStream_t stream);
+// Un-permute gathered tile shards ([nranks][slots][th][tw][3], tile g of the frames x T tiles in
+// rank g % nranks, slot g / nranks) into frames x height x width x 3 bytes.
+void launch_assemble_tiles(const uint8_t *gathered, int32_t width, int32_t height, int32_t tw, int32_t th, int32_t frames,
+                           int32_t nranks, uint8_t *out, hipStream_t stream);
 // rayIntersectTriangle for n (ray, triangle) pairs: R = n x (origin, dest), T = n x 3 vertices
 void launch_ray_triangle_pairs(const float *R, const float *T, int32_t n, uint8_t *hit, float *I, hipStream_t stream);
 

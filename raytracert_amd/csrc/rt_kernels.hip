@@ -2012,6 +2012,25 @@ __global__ __launch_bounds__(kBlock) void k_ray_triangle_pairs(const float *__re
     I[3 * i] = out.x; I[3 * i + 1] = out.y; I[3 * i + 2] = out.z;
 }
 
+// Un-permute of gathered tile shards (multi-GPU frame): gathered = [rank][slot]
+// tiles of tw x th x 3 bytes, global tile id g = f * T + t held by rank g % N in slot g / N; one
+// thread per output pixel of frames x height x width (row-major, 3 bytes each).
+__global__ __launch_bounds__(kBlock) void k_assemble_tiles(const uint8_t *__restrict__ gathered, int32_t width,
+                                                           int32_t height, int32_t tw, int32_t th, int32_t tiles_x,
+                                                           int32_t tiles_total, int32_t nranks, int64_t slots,
+                                                           int64_t npix, uint8_t *__restrict__ out) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= npix) return;
+    const int64_t per_frame = static_cast<int64_t>(width) * height;
+    const int64_t f = i / per_frame, q = i - f * per_frame;
+    const int y = static_cast<int>(q / width), x = static_cast<int>(q - static_cast<int64_t>(y) * width);
+    const int64_t g = f * tiles_total + static_cast<int64_t>(y / th) * tiles_x + x / tw;
+    const int64_t tile = (g % nranks) * slots + g / nranks;
+    const uint8_t *src = gathered + (tile * tw * th + static_cast<int64_t>(y % th) * tw + x % tw) * 3;
+    uint8_t *dst = out + 3 * i;
+    dst[0] = src[0]; dst[1] = src[1]; dst[2] = src[2];
+}
+
 inline unsigned grid_for(int64_t n) { return static_cast<unsigned>((n + kBlock - 1) / kBlock); }
 
 }  // namespace
@@ -2198,6 +2217,16 @@ void launch_face_normals(const float *xyz, const uint32_t *tri_v, int32_t nt, fl
 void launch_ray_triangle_pairs(const float *R, const float *T, int32_t n, uint8_t *hit, float *I, hipStream_t stream) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_ray_triangle_pairs, dim3(grid_for(n)), dim3(kBlock), 0, stream, R, T, n, hit, I);
+}
+
+void launch_assemble_tiles(const uint8_t *gathered, int32_t width, int32_t height, int32_t tw, int32_t th, int32_t frames,
+                           int32_t nranks, uint8_t *out, hipStream_t stream) {
+    const int32_t tiles_x = (width + tw - 1) / tw, tiles_total = tiles_x * ((height + th - 1) / th);
+    const int64_t slots = (static_cast<int64_t>(frames) * tiles_total + nranks - 1) / nranks;
+    const int64_t npix = static_cast<int64_t>(frames) * width * height;
+    if (npix <= 0) return;
+    hipLaunchKernelGGL(k_assemble_tiles, dim3(static_cast<unsigned>((npix + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                       gathered, width, height, tw, th, tiles_x, tiles_total, nranks, slots, npix, out);
 }
 
 }  // namespace rt

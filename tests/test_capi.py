@@ -75,3 +75,17 @@ def test_scene_create_validates_indices():
                        device=R.RT_HOST_ONLY)
     assert s.counts() == (3, 1, 1)
     assert s.export()["normals"].tolist() == [[0.0, 0.0, 1.0]]
+
+
+def test_comm_id_without_gpu_and_init_refusal():
+    """rt_comm_unique_id loads RCCL on first use and makes fresh 128-byte ids; rt_comm_init
+    checks its arguments before any collective (and needs a device)."""
+    a, b = R.Comm.unique_id(), R.Comm.unique_id()
+    assert len(a) == len(b) == _capi.COMM_ID_BYTES and a != b
+    with pytest.raises(R.RtError) as ei:
+        R.Comm(0, 1, 1, a)   # rank outside [0, nranks)
+    assert ei.value.code == _capi.RT_E_ARG
+    if R.device_count() == 0:
+        with pytest.raises(R.RtError) as ei:
+            R.Comm(0, 0, 1, a)
+        assert ei.value.code == _capi.RT_E_NODEV

@@ -1,0 +1,114 @@
+"""The C-ABI multi-GPU path (rt_render_frames_sharded + rt_comm_*, rt_assemble_tiles_device;
+SURVEY.md §8e) on the GPU: the interleaved shards of N simulated ranks, placed as one gather lays
+them out and un-permuted by the library, equal the one-GPU frame for N = 2, 3, 5 and multi-frame
+batches; a world-1 RCCL communicator renders through the real gather; with two or more GPUs
+visible, two processes render one frame over RCCL."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import raytracert_amd as R
+from _util import scene_path
+
+pytestmark = pytest.mark.gpu
+
+LIGHTS = [(0.0, 0.0, 4.0), (1.5, 1.5, 4.0)]
+
+
+def _frame(sc, p):
+    import torch
+    fb = torch.zeros(p.height * p.width * 3, dtype=torch.uint8, device="cuda:0")
+    c = sc.render_frame_device(p, 16, 16, fb.data_ptr(), fb.numel(), torch.cuda.current_stream().cuda_stream,
+                               want_counts=True)
+    return fb.view(p.height, p.width, 3).cpu().numpy(), c
+
+
+@pytest.mark.parametrize("nranks,frames,size,tile", [(2, 1, (100, 70), 16), (3, 2, (100, 70), 16), (5, 3, (61, 29), 8),
+                                                     (3, 1, (1920, 1080), 16)])
+def test_assemble_composes_interleaved_shards(nranks, frames, size, tile, workdir, gpu_available):
+    import torch
+    w, h = size
+    p = R.RenderParams(width=w, height=h, pf=1, max_lvl=3, lights=LIGHTS)
+    T = ((w + tile - 1) // tile) * ((h + tile - 1) // tile)
+    slots = (frames * T + nranks - 1) // nranks
+    shard = slots * tile * tile * 3
+    stream = torch.cuda.current_stream().cuda_stream
+    with R.Scene.load(scene_path("syn:C4" if w > 1000 else "syn:F3", workdir), device=0) as sc:
+        full, c1 = _frame(sc, R.RenderParams(width=w, height=h, pf=1, max_lvl=3, lights=LIGHTS))
+        gathered = torch.full((nranks * shard,), 9, dtype=torch.uint8, device="cuda:0")
+        total = np.zeros(3, np.uint64)
+        for r in range(nranks):   # what one gather of equal-sized shards lays out
+            part = gathered[r * shard:(r + 1) * shard]
+            n, c = sc.render_tiles_device(p, tile, tile, r, nranks, part.data_ptr(), part.numel(), stream,
+                                          want_counts=True, frames=frames)
+            assert n == (frames * T - r + nranks - 1) // nranks
+            total += c
+        out = torch.zeros(frames * h * w * 3, dtype=torch.uint8, device="cuda:0")
+        R.assemble_tiles_device(0, w, h, tile, tile, frames, nranks, gathered.data_ptr(), gathered.numel(), out.data_ptr(),
+                                out.numel(), stream)
+        frames_out = out.view(frames, h, w, 3).cpu().numpy()
+    for f in range(frames):
+        assert np.array_equal(frames_out[f], full), f
+    assert [int(x) for x in total] == [frames * int(x) for x in c1]
+
+
+def test_render_frames_sharded_world1(workdir, gpu_available):
+    import torch
+    comm = R.Comm(0, 0, 1, R.Comm.unique_id())
+    assert comm.info() == (0, 1, 0)
+    p = R.RenderParams(width=320, height=180, pf=2, max_lvl=3, lights=LIGHTS)
+    with R.Scene.load(scene_path("syn:C4", workdir), device=0) as sc:
+        full, c1 = _frame(sc, p)
+        for frames in (1, 2):
+            out = torch.zeros(frames * 180 * 320 * 3, dtype=torch.uint8, device="cuda:0")
+            c = sc.render_frames_sharded(p, comm, 16, 16, frames, out.data_ptr(), out.numel(),
+                                         torch.cuda.current_stream().cuda_stream, want_counts=True)
+            got = out.view(frames, 180, 320, 3).cpu().numpy()
+            for f in range(frames):
+                assert np.array_equal(got[f], full)
+            assert [int(x) for x in c] == [frames * int(x) for x in c1]
+        with pytest.raises(R.RtError):   # rank 0 must pass an output buffer
+            sc.render_frames_sharded(p, comm, 16, 16, 1, None, 0)
+    comm.check()
+    comm.close()
+
+
+WORKER = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [sys.argv[5], sys.argv[5] + "/tests"]
+import raytracert_amd as R
+from _util import scene_path
+rank, n, uid_file, out_file = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+torch.cuda.set_device(rank)
+comm = R.Comm(rank, rank, n, open(uid_file, "rb").read())
+sc = R.Scene.load(scene_path("syn:F3", "/tmp/rt_sharded_%d" % rank), device=rank)
+p = R.RenderParams(width=100, height=70, pf=2, max_lvl=3, lights=[(0.0, 0.0, 4.0), (1.5, 1.5, 4.0)])
+out = torch.zeros(2 * 70 * 100 * 3, dtype=torch.uint8, device="cuda:%d" % rank)
+c = sc.render_frames_sharded(p, comm, 16, 16, 2, out.data_ptr() if rank == 0 else None, out.numel() if rank == 0 else 0,
+                             torch.cuda.current_stream().cuda_stream, want_counts=True)
+if rank == 0:
+    np.save(out_file, out.cpu().numpy())
+comm.close()
+"""
+
+
+def test_render_frames_sharded_two_processes(workdir, tmp_path, gpu_available):
+    if gpu_available < 2:
+        pytest.skip("one GPU visible: RCCL refuses two ranks on one device (covered by the composition test)")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    uid = tmp_path / "uid"
+    uid.write_bytes(R.Comm.unique_id())
+    script = tmp_path / "worker.py"
+    script.write_text(WORKER)
+    out = str(tmp_path / "frames.npy")
+    env = dict(os.environ)
+    procs = [subprocess.Popen([sys.executable, str(script), str(r), "2", str(uid), out, root], env=env) for r in range(2)]
+    assert [p.wait(timeout=180) for p in procs] == [0, 0]
+    p = R.RenderParams(width=100, height=70, pf=2, max_lvl=3, lights=LIGHTS)
+    with R.Scene.load(scene_path("syn:F3", workdir), device=0) as sc:
+        full, _ = _frame(sc, p)
+    got = np.load(out).reshape(2, 70, 100, 3)
+    assert np.array_equal(got[0], full) and np.array_equal(got[1], full)

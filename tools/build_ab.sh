@@ -13,7 +13,7 @@ done
 wait
 for o in ab/k_*.o; do
   N=${o#ab/k_}; N=${N%.o}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -pthread -o ab/lib_$N.so $o build/rt_capi.o build/scene_loader.o build/obj_parallel.o build/bvh.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -pthread -o ab/lib_$N.so $o build/rt_capi.o build/rt_comm.o build/scene_loader.o build/obj_parallel.o build/bvh.o -ldl
   rm -f $o
 done
 ls ab
