@@ -77,7 +77,7 @@ def test_dropin_frame_loop_equals_render_and_oracle(spec, w, h, pf, lvl, dropin_
     _, ou8, oc = O.OracleScene(path).render(O.make_params(w, h, pf, lvl, lights=lights), nthreads=16)
     d = np.abs(a.astype(np.int16) - ou8.astype(np.int16))
     assert d.max() <= 1 and (d == 0).mean() >= 0.9999
-    assert out["rays"] == [str(int(x)) for x in oc]
+    assert out["frames"][2] == "rays" and out["frames"][3:6] == [str(int(x)) for x in oc]
     assert out["centre"][4] == "1" or out["centre"][0] == "-1"          # the hit triangle's own test agrees
     if out["centre"][0] != "-1":
         assert out["centre"][5] == "1"

@@ -8,7 +8,7 @@ import pytest
 
 import oracle as O
 import raytracert_amd as R
-from _util import scene_path
+from _util import scene_path, write_adversarial_obj
 
 
 def _same(a, b):
@@ -120,45 +120,7 @@ def test_parallel_loader_adversarial(tmp_path):
     malformed `v` lines (x, y, z persist from the previous line), hex/inf/nan/long-digit numbers,
     exponents at the fast path's edges, usemtl before mtllib and of unknown names, n-gons,
     v/t/n tokens, tabs, CRLF, a NUL byte and no trailing newline."""
-    d = str(tmp_path)
-    _write(d, "a.mtl", "newmtl A\nKd 1 0 0\n\nnewmtl B\nKd 0 1 0\nd 0.5\n\n")
-    _write(d, "b.mtl", "newmtl C\nKd 0 0 1\n\n")
-    rng = np.random.default_rng(7)
-    lines = ["# adversarial", "usemtl A", "mtllib a.mtl"]
-    spellings = ["1", "-2.5", "+3.25", ".5", "5.", "1e3", "1E-3", "-0.000000", "0.1234567", "123456789.125",
-                 "0.12345678901234567890123", "3.4028235e38", "1e39", "1e-40", "1.17549435e-38", "0x1.8p1",
-                 "inf", "-infinity", "nan", "1e", "1e+", "1,5", "7abc", "00012.5000", "9999999", "16777217",
-                 "1e10", "1e-10", "1e11", "2.5e-11"]
-    for i in range(3000):
-        r = rng.random()
-        if r < 0.55:
-            k = rng.integers(0, 4)
-            toks = [spellings[rng.integers(0, len(spellings))] if rng.random() < 0.3 else "%.6f" % rng.normal()
-                    for _ in range(k)]
-            sep = " \t " if rng.random() < 0.1 else " "
-            lines.append("v " + sep.join(toks))
-        elif r < 0.85:
-            n = int(rng.integers(1, 7))
-            idx = rng.integers(-2, max(3, len(lines) // 2), n)
-            form = rng.integers(0, 3)
-            toks = [str(v) if form == 0 else ("%d/%d/%d" % (v, v, v) if form == 1 else "%d//%d" % (v, v)) for v in idx]
-            lines.append("f " + " ".join(toks))
-        elif r < 0.88:
-            lines.append("usemtl " + ["A", "B", "C", "Nope"][rng.integers(0, 4)])
-        elif r < 0.89:
-            lines.append("mtllib b.mtl" if rng.random() < 0.5 else "mtllib a.mtl")
-        elif r < 0.93:   # > 255 characters: later fgets chunks start mid-line
-            lines.append("v " + " ".join("%.9f" % x for x in rng.normal(size=int(rng.integers(20, 40)))))
-        elif r < 0.95:
-            lines.append("f " + " ".join(str(int(x)) for x in rng.integers(1, 50, int(rng.integers(60, 120)))))
-        elif r < 0.97:
-            lines.append("#" + "x" * int(rng.integers(200, 600)))
-        else:
-            lines.append(["vt 0 0", "vn 0 0 1", "o thing", "g grp", "s off", "", "   v 1 2 3", "\tf 1 2 3",
-                          "v", "f", "vx 1 2 3"][rng.integers(0, 11)])
-    text = "\r\n".join(lines[:1500]) + "\r\n" + "\n".join(lines[1500:])
-    text = text.replace("v 1 2 3", "v 1\x00 2 3", 1) + "\nv 4 5 6\nf 1 2 3"   # NUL byte, no final newline
-    p = _write(d, "adv.obj", text)
+    p = write_adversarial_obj(str(tmp_path))
     seq = _loaders_agree(p)
     # default + A + B: every later mtllib appends to the already-extended prefix (mesh.cpp:173-175)
     # and names a file that does not exist, so C is never defined
