@@ -64,6 +64,7 @@ struct DevScene {
     // BVH (use_bvh != 0): nodes, leaf-ordered records and their original indices, always list
     const BvhNode *nodes;
     const TriRec *leaf_recs;
+    const float4 *leaf48;           // the leaf records as {T0, u, v, n}, 3 x float4 each (RT_LEAF48)
     const uint32_t *leaf_idx;
     const uint32_t *always;
     const TriRec *always_recs;      // the always list's records, contiguous

@@ -154,6 +154,28 @@ __device__ __forceinline__ void test_triangle(const TriRec &T, int t, V3 o, V3 d
     }
 }
 
+// A leaf record of the BVH: the 64-B TriRec, or (RT_LEAF48, A/B) the 48-B {T0, u, v, n} with
+// uu, uv, vv and D recomputed here in the host's order (scene_loader.cpp build_tri_records, the
+// reference's :134-136,140): the same binary32 operations, so the same bits.
+#ifndef RT_LEAF48
+#define RT_LEAF48 0
+#endif
+__device__ __forceinline__ TriRec leaf_rec(const DevScene &sc, int i) {
+    if (!RT_LEAF48) return sc.leaf_recs[i];
+    const float4 *q = sc.leaf48 + 3 * static_cast<int64_t>(i);
+    const float4 a = q[0], b = q[1], c = q[2];
+    TriRec T;
+    T.t0[0] = a.x; T.t0[1] = a.y; T.t0[2] = a.z;
+    T.u[0] = a.w; T.u[1] = b.x; T.u[2] = b.y;
+    T.v[0] = b.z; T.v[1] = b.w; T.v[2] = c.x;
+    T.n[0] = c.y; T.n[1] = c.z; T.n[2] = c.w;
+    T.uu = T.u[0] * T.u[0] + T.u[1] * T.u[1] + T.u[2] * T.u[2];
+    T.uv = T.u[0] * T.v[0] + T.u[1] * T.v[1] + T.u[2] * T.v[2];
+    T.vv = T.v[0] * T.v[0] + T.v[1] * T.v[1] + T.v[2] * T.v[2];
+    T.D = T.uv * T.uv - T.uu * T.vv;
+    return T;
+}
+
 // Scalar-load pipeline: records A and B alternate; each is fenced (s_waitcnt) before the next
 // record's s_load is issued, so one load is always in flight behind the arithmetic.
 template <bool kAnyHit>
@@ -242,9 +264,12 @@ __device__ __forceinline__ LaneStack lane_stack(const DevScene &sc, int32_t *lds
 }
 
 // A four-wide node's 64 bytes: from the LDS copy for the top levels, else from the node array.
+#ifndef RT_TOP_LDS
+#define RT_TOP_LDS 1   // 0 (A/B): no LDS node cache, so node loads are global loads, not flat ones
+#endif
 __device__ __forceinline__ void load_node4(const LaneStack &stack, const Bvh4Node *__restrict__ nodes4, int32_t ref,
                                            uint4 &a, uint4 &b, uint4 &c, uint4 &d) {
-    if (ref < stack.ntop) {
+    if (RT_TOP_LDS && ref < stack.ntop) {
         const uint4 *p = stack.top + 4 * ref;
         a = p[0]; b = p[1]; c = p[2]; d = p[3];
     } else {
@@ -306,15 +331,15 @@ __device__ __forceinline__ void test_leaf(const DevScene &sc, int first, int cnt
         // does not depend on the order of the tests.
         for (int k = 0; k < cnt; k += 2) {
             const int k1 = min(k + 1, cnt - 1);
-            const TriRec A = sc.leaf_recs[first + k];
-            const TriRec B = sc.leaf_recs[first + k1];
+            const TriRec A = leaf_rec(sc, first + k);
+            const TriRec B = leaf_rec(sc, first + k1);
             test_triangle<kAnyHit, true>(A, static_cast<int>(sc.leaf_idx[first + k]), o, dir, best, bidx, bI, done);
             if (k1 != k) test_triangle<kAnyHit, true>(B, static_cast<int>(sc.leaf_idx[first + k1]), o, dir, best, bidx, bI, done);
         }
         return;
     }
     for (int k = 0; k < cnt; ++k) {
-        const TriRec T = sc.leaf_recs[first + k];
+        const TriRec T = leaf_rec(sc, first + k);
         test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first + k]), o, dir, best, bidx, bI, done);
     }
 }
@@ -552,7 +577,7 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
 #ifdef RT_STAMPS
                 for (int k = 0; k < cnt; ++k) {
                     RT_STAMP(s0);
-                    const TriRec T = sc.leaf_recs[first + k];
+                    const TriRec T = leaf_rec(sc, first + k);
                     asm volatile("" ::"v"(T.t0[0]), "v"(T.u[0]), "v"(T.v[0]), "v"(T.n[0]));
                     RT_STAMP(s1);
                     test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first + k]), o, dir, best, bidx, bI, done);
@@ -753,7 +778,7 @@ __device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, 
             if (RT_WW_CURSOR) {
                 // one triangle per iteration: the ref is the cursor (first + 1, count - 1), so a lane
                 // whose leaf ends goes on to its next leaf while the others test their next triangle
-                const TriRec T = sc.leaf_recs[first];
+                const TriRec T = leaf_rec(sc, first);
                 test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first]), o, dir, best, bidx, bI, done);
                 ++tests;
                 if (kAnyHit && done) { node = kDoneRef; leaf2 = kDoneRef; break; }
@@ -892,7 +917,7 @@ __device__ __forceinline__ void bvh4_query_pair(const DevScene &sc, V3 o, PairRa
             const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
             const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
             for (int k = 0; k < cnt; ++k) {
-                const TriRec T = sc.leaf_recs[first + k];
+                const TriRec T = leaf_rec(sc, first + k);
                 const int t = static_cast<int>(sc.leaf_idx[first + k]);
                 test_triangle<kAnyHit, true>(T, t, o, r0.dir, r0.best, r0.bidx, dummy, r0.done);
                 test_triangle<kAnyHit, true>(T, t, o, r1.dir, r1.best, r1.bidx, dummy, r1.done);
@@ -1481,7 +1506,20 @@ struct Secondary {
     V3 coef;
     V3 org, dst;
     int lvl;
+    V3 local;           // this step's local colour (shade's sum before the child's term)
+    uint32_t code;      // in-lane chain records: state | coefficient kind << 2 | material << 3
 };
+
+// In-lane chain (RT_CHAIN_INLANE, the fused chain launch): a step's record is written only when
+// the step has a child, as 16 B {local colour, code}, where the code names the child's coefficient
+// by the hit material (kind 0: Ks, reflection and the acos branch of refraction; kind 1: (1 - Tr)
+// broadcast, transmission: raytracing.cpp:298-328,361-363), so the fold re-derives the same floats;
+// the chain's last step stays in registers and the lane folds its chain itself.
+#ifndef RT_CHAIN_INLANE
+#define RT_CHAIN_INLANE 1   // measured neutral in time (C4 0.499 vs 0.500-0.51 ms, C5 grid 0.65 both) with
+                            // fewer bytes written and read back; bit-identical frames
+#endif
+constexpr uint32_t kCoefTr = 4u;
 
 // A chain record store. RT_CHAIN_SC1 (A/B build): written through past L2 (sc1), so the records,
 // read back once when the chain is folded, do not evict scene lines from the XCD's L2.
@@ -1529,7 +1567,7 @@ __device__ __forceinline__ void offset_point(V3 &point, V3 dest) {   // addOffse
 // record (local colour and child state, the child's coefficient, the depth when the chain ends)
 // and returns the secondary ray, if any. ray = dest - origin of the traced ray (:393);
 // is_shadowed(l) is isShadow's verdict for light l.
-template <typename Shadowed>
+template <bool kInLane = false, typename Shadowed>
 __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadeParams &p, const DevWork &w, int step,
                                                int sample, V3 ray, int lvl, int idx, V3 P,
                                                Shadowed &&is_shadowed) {
@@ -1540,7 +1578,9 @@ __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadePa
     sec.lvl = -1;
     const int64_t ci = static_cast<int64_t>(step) * w.cap + sample;
     V3 normal = ld3(sc.normals[idx]);                                // :394 (copy, mutated below)
-    const DevMaterial m = sc.mats[sc.tri_mat[idx]];                  // :396
+    const uint32_t mi = sc.tri_mat[idx];
+    const DevMaterial m = sc.mats[mi];                               // :396
+    uint32_t kind = 0;
     const V3 Kd = mk(m.Kd[0], m.Kd[1], m.Kd[2]);
     const V3 Ka = mk(m.Ka[0], m.Ka[1], m.Ka[2]);
     const V3 Ks = mk(m.Ks[0], m.Ks[1], m.Ks[2]);
@@ -1596,6 +1636,7 @@ __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadePa
                     sec.state = kChildTrace; sec.lvl = rl + 1;
                     const float c = 1 - m.Tr;
                     sec.coef = mk(c, c, c);
+                    kind = kCoefTr;
                 }
             }
         } else {
@@ -1611,16 +1652,38 @@ __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadePa
                 sec.state = kChildTrace; sec.lvl = rl + 1;
                 const float c = 1 - m.Tr;
                 sec.coef = mk(c, c, c);
+                kind = kCoefTr;
             }
         }
     } else if ((f & RT_REFLECTION) && lvl < p.max_lvl) {            // :361-363
         sec.state = kChildTrace; sec.coef = Ks; sec.lvl = lvl + 1;
         reflection_ray(ray, P, normal, sec.org, sec.dst);
     }
+    sec.local = color;
+    sec.code = sec.state | kind | (mi << 3);
+    if (kInLane) {   // the caller keeps the chain (records of the steps with a child only)
+        if (sec.state == kChildTrace) store_chain(&w.chain_local[ci], make_float4(color.x, color.y, color.z, as_float(static_cast<int>(sec.code))));
+        return sec;
+    }
     store_chain(&w.chain_local[ci], make_float4(color.x, color.y, color.z, as_float(static_cast<int>(sec.state))));
     if (sec.state == kChildTrace) store_chain(&w.chain_coef[ci], make_float4(sec.coef.x, sec.coef.y, sec.coef.z, 0.0f));
     else w.depth[sample] = static_cast<uint8_t>(step + 1);
     return sec;
+}
+
+// The in-lane fold: the last step's colour c (its state applied) through the stored records of the
+// steps first..last-1 back to front, c_k = local_k + coef_k * c_{k+1} (fold_chain's arithmetic).
+__device__ __forceinline__ V3 fold_inlane(const DevScene &sc, const DevWork &w, int first, int last, int sample, V3 c) {
+    for (int k = last - 1; k >= first; --k) {
+        const float4 L = w.chain_local[static_cast<int64_t>(k) * w.cap + sample];
+        const uint32_t code = static_cast<uint32_t>(as_int(L.w));
+        const DevMaterial &m = sc.mats[code >> 3];
+        V3 K;
+        if (code & kCoefTr) { const float t = 1 - m.Tr; K = mk(t, t, t); }
+        else K = mk(m.Ks[0], m.Ks[1], m.Ks[2]);
+        c = add(mk(L.x, L.y, L.z), mul(K, c));
+    }
+    return c;
 }
 
 // trace() miss (:389-391): black, and the chain ends at this step.
@@ -1707,13 +1770,14 @@ __device__ __forceinline__ void store_pixel(V3 rgb, int64_t o, uint8_t *__restri
 
 constexpr int kChainSteps = 256;   // max_lvl <= 254
 #ifndef RT_CHAIN_WPE
-#define RT_CHAIN_WPE 6   // measured: 6 (80 VGPRs, 36 B spill) beats 5 (92, none) and 7
+#define RT_CHAIN_WPE 5   // r02, with in-lane chains: 5 (0.493-0.499 ms) vs 6 (0.533, more spills) vs 4 (0.51);
+                         // r01, before them: 6 (80 VGPRs, 36 B spill) beat 5 (92, none) and 7
 #endif
 
 // One chain step of one sample (trace, raytracing.cpp:381-406): the closest-hit query, isShadow
 // per light (:241-261), shade (:335-368). Returns the secondary ray (state kChildTrace) or the end
 // of the chain. Shadow-ray statistics are counted per block in s_sh.
-template <bool kAnyHit, int W, bool kCount>
+template <bool kAnyHit, int W, bool kCount, bool kInLane = false>
 __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeParams &p, const DevWork &w, int step,
                                                 int sample, V3 org, V3 dst, int lvl, const LaneStack &stack,
                                                 int32_t *lds_stack, const Bvh4Node *__restrict__ n4,
@@ -1721,11 +1785,15 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
                                                 int *s_sh, WorkTally<kCount> &wc, WorkTally<kCount> &ws) {
     Secondary none;
     none.state = kChildNone;
+    none.local = mk(0, 0, 0);   // trace() miss: black (:389-391)
     int bidx = -1;
     V3 bI = mk(0, 0, 0);
     bvh_query_w<false, W>(sc, n4, lrec, lidx, lds_stack, org, sub(dst, org), true, bidx, bI, stack, wc.tests, wc.visits);
     if (bidx >= sc.nt) { w.counters[kErrorSlot] = 1; bidx = -1; }
-    if (bidx < 0) { shade_miss(w, step, sample); return none; }
+    if (bidx < 0) {
+        if (!kInLane) shade_miss(w, step, sample);
+        return none;
+    }
     uint32_t mask = 0;   // isShadow per light (:241-261)
     const bool shadows = (p.flags & RT_SHADOWS) && p.n_lights > 0;
     if (shadows) {
@@ -1753,7 +1821,7 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
             if (sidx >= 0 && !sc.mats[sc.tri_mat[sidx]].transparent) mask |= 1u << l;   // :253-257
         }
     }
-    return shade_hit(sc, p, w, step, sample, sub(dst, org), lvl, bidx, bI, [&](int l) { return ((mask >> l) & 1u) != 0; });
+    return shade_hit<kInLane>(sc, p, w, step, sample, sub(dst, org), lvl, bidx, bI, [&](int l) { return ((mask >> l) & 1u) != 0; });
 }
 
 // Chain tail (RT_TUNE_CHAIN_FROM): the remaining steps of every query in Q_first, each lane
@@ -1766,7 +1834,7 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
 // w.batch_order[v]; every wave records its batch's duration in w.batch_cost, from which
 // launch_order_batches prepares the next launch's order (longest first, so the deep reflection
 // chains of a frame start at once instead of trailing it). Placement never changes results.
-template <int W, bool kAnyHit, bool kCount>
+template <int W, bool kAnyHit, bool kCount, bool kInLane = false>
 __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CHAIN_WPE))) void k_chain(
     const DevScene sc, const ShadeParams p, DevWork w, int first, const Bvh4Node *__restrict__ n4,
     const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx, int ordered, uint8_t *__restrict__ out_u8,
@@ -1803,14 +1871,19 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
         V3 org = mk(qo.x, qo.y, qo.z), dst = mk(qd.x, qd.y, qd.z);
         for (int step = first; step < kChainSteps; ++step) {
             if (step > first) atomicAdd(&s_q[step], 1);
-            const Secondary sec = chain_step<kAnyHit, W>(sc, p, w, step, sample, org, dst, lvl, stack, lds_stack, n4, lrec,
-                                                         lidx, s_sh, wc, ws);
-            if (sec.state != kChildTrace) break;
+            const Secondary sec = chain_step<kAnyHit, W, kCount, kInLane>(sc, p, w, step, sample, org, dst, lvl, stack,
+                                                                          lds_stack, n4, lrec, lidx, s_sh, wc, ws);
+            if (sec.state != kChildTrace) {
+                if (kInLane)   // the chain ends here: fold it in the lane (fold_chain's arithmetic)
+                    rgb = fold_inlane(sc, w, first, step, sample,
+                                      sec.state == kChildZero ? add(sec.local, mk(0.0f, 0.0f, 0.0f)) : sec.local);
+                break;
+            }
             org = sec.org;
             dst = sec.dst;
             lvl = sec.lvl;
         }
-        if (fuse_spp) { rgb = fold_chain(w, sample); px = w.pix_out[sample]; }
+        if (fuse_spp) { if (!kInLane) rgb = fold_chain(w, sample); px = w.pix_out[sample]; }
         }(ordered ? pb * kWave + (j0 & (kWave - 1)) : j0);
         if (fuse_spp) {   // k_frame's arithmetic: a pixel's fuse_spp sub-samples sit in adjacent lanes
             const int lane = __lane_id(), base = lane & ~(fuse_spp - 1);
@@ -2161,8 +2234,16 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
     const DevScene s = for_width(s0, wide ? 4 : 2);
     auto k = wide ? (s.any_transparent ? k_chain<4, false, false> : k_chain<4, true, false>)
                   : (s.any_transparent ? k_chain<2, false, false> : k_chain<2, true, false>);
+    // fused pixel writes from step 0: each lane folds its own chain (RT_CHAIN_INLANE)
+    const bool inlane = RT_CHAIN_INLANE && fuse_spp > 0 && first == 0;
+    if (inlane)
+        k = wide ? (s.any_transparent ? k_chain<4, false, false, true> : k_chain<4, true, false, true>)
+                 : (s.any_transparent ? k_chain<2, false, false, true> : k_chain<2, true, false, true>);
 #ifndef RT_WAVE_TIMES   // (the wave-times diagnostic build times the uncounted kernel)
-    if (s.work)
+    if (s.work && inlane)
+        k = wide ? (s.any_transparent ? k_chain<4, false, true, true> : k_chain<4, true, true, true>)
+                 : (s.any_transparent ? k_chain<2, false, true, true> : k_chain<2, true, true, true>);
+    else if (s.work)
         k = wide ? (s.any_transparent ? k_chain<4, false, true> : k_chain<4, true, true>)
                  : (s.any_transparent ? k_chain<2, false, true> : k_chain<2, true, true>);
 #endif

@@ -17,12 +17,15 @@ import raytracert_amd as R  # noqa: E402
 from raytracert_amd import scenes  # noqa: E402
 
 knobs = json.loads(sys.argv[1]) if len(sys.argv) > 1 else {}
-obj = scenes.write_sphere_grid(scenes.C4, tempfile.mkdtemp(), "wt")
+import bench  # noqa: E402  (WORKLOAD=c2|c3|c4|c5: the bench's configurations)
+wl = bench.WORKLOADS[os.environ.get("WORKLOAD", "c4")]
+obj = bench.workload_scene(wl["scene"], tempfile.mkdtemp())
 sc = R.Scene.load(obj, device=0)
 sc.tune("pipes", 1)
 for k, v in knobs.items():
     sc.tune(k, v)
-p = R.RenderParams(width=1920, height=1080, pf=1, max_lvl=int(os.environ.get("MAX_LVL", "3")), lights=[[0, 0, 4], [1.5, 1.5, 4]])
+p = R.RenderParams(width=wl["width"], height=wl["height"], pf=wl["pf"], max_lvl=int(os.environ.get("MAX_LVL", wl["max_lvl"])),
+                   lights=wl["lights"])
 sc.render(p)
 sc.reset_stats()
 sc.set_profiling(True, count_work=True)
