@@ -78,6 +78,7 @@ def test_dropin_frame_loop_equals_render_and_oracle(spec, w, h, pf, lvl, dropin_
     d = np.abs(a.astype(np.int16) - ou8.astype(np.int16))
     assert d.max() <= 1 and (d == 0).mean() >= 0.9999
     assert out["frames"][2] == "rays" and out["frames"][3:6] == [str(int(x)) for x in oc]
-    assert out["centre"][4] == "1" or out["centre"][0] == "-1"          # the hit triangle's own test agrees
-    if out["centre"][0] != "-1":
-        assert out["centre"][5] == "1"
+    c = out["centre"]   # idx, I (3 words), "tri_hit", hit, "same_point", same
+    assert c[4] == "tri_hit" and c[6] == "same_point"
+    if c[0] != "-1":   # rayIntersectTriangle on intersectMesh's triangle: a hit at the same point
+        assert c[5] == "1" and c[7] == "1"
