@@ -477,8 +477,13 @@ def pmc_traffic(kernel: str):
         except (OSError, ValueError):
             continue
         ks = d.get("kernels", {})
-        # the timed (non-counting) instantiation of the kernel, e.g. "k_bvh_closest_hit<4, false>"
-        names = [n for n in ks if n == kernel or (n.startswith(kernel + "<") and n.endswith("false>"))]
+        # the timed (non-counting) instantiation of the kernel: kCount is the third template argument
+        # of k_chain<W, kAnyHit, kCount, kInLane>, the last one of k_bvh_closest_hit<W, kCount>
+        def counting(n):
+            args = [a.strip() for a in n[n.index("<") + 1:n.rindex(">")].split(",")]
+            return args[2] if kernel == "k_chain" and len(args) > 2 else args[-1]
+        names = [n for n in ks if n == kernel or (n.startswith(kernel + "<") and counting(n) == "false")]
+        names.sort(key=lambda n: -ks[n].get("launches_in_pass", 0))
         for n in names:
             if "traffic_bytes_per_launch" in ks[n]:
                 return ks[n]["traffic_bytes_per_launch"], os.path.relpath(f, HERE)
