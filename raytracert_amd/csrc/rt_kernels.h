@@ -127,9 +127,12 @@ void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *
 // fuse_spp > 0 (first == 0, after launch_gen_primary(fused); fuse_spp = samples per pixel, a divisor
 // of 64): each wave writes its pixels into out_u8/out_f32 when its batch's chains end, with
 // k_frame's arithmetic, so no k_frame follows.
+// g (fused launches from step 0): the batch's frame geometry; in-lane chain kernels then make their
+// primary rays themselves (launch_gen_primary(fused) only resets the counters; primaries_inline()).
 void launch_chain(const DevScene &s, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
                   hipStream_t stream, bool ordered = false, uint8_t *out_u8 = nullptr, float *out_f32 = nullptr,
-                  int fuse_spp = 0);
+                  int fuse_spp = 0, const FrameGeom *g = nullptr);
+bool primaries_inline();
 void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t stream);
 // Batch order: the chain launch's 64-sample batches sorted by the durations it measured, longest
 // first (w.batch_cost -> w.batch_order); the next launch over the same batches dispatches in that

@@ -1405,29 +1405,20 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
     return h;
 }
 
-// Also resets the batch's queue counters and work-queue slots (counter 0 = the queue's size), so
-// no separate fills precede the batch. fused (the chain launch writes the pixels): also records each sample's pixel index in w.pix_out and writes the pixels outside the
-// frame black in the tile-major layout, as k_frame does.
-__global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWork w, uint8_t *__restrict__ fused_u8,
-                                                        int fused) {
+// Sample s of a batch (main.cpp:355-395 for one sub-sample): its pixel, its output index px (the
+// tile-major shard slot or the row-major index in the clip rectangle) and its primary ray; false for
+// samples outside the frame or the clip rectangle (origin and dest then (0,0,0)).
+__device__ __forceinline__ bool primary_sample(const FrameGeom &g, int64_t s, V3 &origin, V3 &dest, int64_t &px, int &sub) {
     const int spp = g.pfx * g.pfy;
-    const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th * spp;
-    const int64_t s = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (s < 2 * kMaxStepsCounters) w.counters[s] = s == 0 ? static_cast<int32_t>(n) : 0;
-    if (s < 2 * static_cast<int64_t>(w.steps) * kWqSlot) w.wq[s] = 0;
-    if (s >= n) return;
     const int64_t pix = s / spp;
-    const int sub = static_cast<int>(s - pix * spp);
+    sub = static_cast<int>(s - pix * spp);
     const int subx = sub / g.pfy, suby = sub - subx * g.pfy;   // subx outer, suby inner (:377-378)
     int x, y;
     const bool valid = decode_pixel(g, pix, x, y);
-    if (fused) {
-        const int64_t px = g.out_mode == 0 ? static_cast<int64_t>(g.tile0) * g.tw * g.th + pix
-                                           : static_cast<int64_t>(y - g.oy) * g.cw + (x - g.ox);
-        if (valid) w.pix_out[s] = static_cast<int32_t>(px);
-        else if (g.out_mode == 0 && fused_u8 && sub == 0) { fused_u8[3 * px] = 0; fused_u8[3 * px + 1] = 0; fused_u8[3 * px + 2] = 0; }
-    }
-    V3 origin = mk(0, 0, 0), dest = mk(0, 0, 0);
+    px = g.out_mode == 0 ? static_cast<int64_t>(g.tile0) * g.tw * g.th + pix
+                         : static_cast<int64_t>(y - g.oy) * g.cw + (x - g.ox);
+    origin = mk(0, 0, 0);
+    dest = mk(0, 0, 0);
     if (valid) {
         float fx = static_cast<float>(subx), fy = static_cast<float>(suby);
         if (g.stochastic) {   // RT_STOCHASTIC (include/raytracert.h): jitter inside the grid cell
@@ -1453,6 +1444,30 @@ __global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWo
                      scale(add(scale(o01, xscale), scale(o11, ix)), iy));                     // :383-384
         dest = add(scale(add(scale(d00, xscale), scale(d10, ix)), yscale),
                    scale(add(scale(d01, xscale), scale(d11, ix)), iy));                       // :385-386
+    }
+    return valid;
+}
+
+// Also resets the batch's queue counters and work-queue slots (counter 0 = the queue's size), so
+// no separate fills precede the batch. fused 1 (the chain launch writes the pixels): also records
+// each sample's pixel index in w.pix_out and writes the pixels outside the frame black in the
+// tile-major layout, as k_frame does. fused 2 (RT_PRIMARY_INLINE): the resets only; the chain
+// launch makes each primary ray in its lane (primary_sample) and writes those pixels itself.
+__global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWork w, uint8_t *__restrict__ fused_u8,
+                                                        int fused) {
+    const int spp = g.pfx * g.pfy;
+    const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th * spp;
+    const int64_t s = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (s < 2 * kMaxStepsCounters) w.counters[s] = s == 0 ? static_cast<int32_t>(n) : 0;
+    if (s < 2 * static_cast<int64_t>(w.steps) * kWqSlot) w.wq[s] = 0;
+    if (s >= n || fused == 2) return;   // 2: the chain launch generates its primaries itself
+    V3 origin, dest;
+    int64_t px;
+    int sub;
+    const bool valid = primary_sample(g, s, origin, dest, px, sub);
+    if (fused) {
+        if (valid) w.pix_out[s] = static_cast<int32_t>(px);
+        else if (g.out_mode == 0 && fused_u8 && sub == 0) { fused_u8[3 * px] = 0; fused_u8[3 * px + 1] = 0; fused_u8[3 * px + 2] = 0; }
     }
     w.depth[s] = 0;
     w.q_org[0][s] = make_float4(origin.x, origin.y, origin.z, as_float(static_cast<int>(s)));
@@ -1515,6 +1530,9 @@ struct Secondary {
 // by the hit material (kind 0: Ks, reflection and the acos branch of refraction; kind 1: (1 - Tr)
 // broadcast, transmission: raytracing.cpp:298-328,361-363), so the fold re-derives the same floats;
 // the chain's last step stays in registers and the lane folds its chain itself.
+#ifndef RT_PRIMARY_INLINE
+#define RT_PRIMARY_INLINE 1   // in-lane chain launches make their primary rays themselves (no primary queue)
+#endif
 #ifndef RT_CHAIN_INLANE
 #define RT_CHAIN_INLANE 1   // measured neutral in time (C4 0.499 vs 0.500-0.51 ms, C5 grid 0.65 both) with
                             // fewer bytes written and read back; bit-identical frames
@@ -1838,7 +1856,8 @@ template <int W, bool kAnyHit, bool kCount, bool kInLane = false>
 __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CHAIN_WPE))) void k_chain(
     const DevScene sc, const ShadeParams p, DevWork w, int first, const Bvh4Node *__restrict__ n4,
     const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx, int ordered, uint8_t *__restrict__ out_u8,
-    float *__restrict__ out_f32, int fuse_spp) {
+    float *__restrict__ out_f32, int fuse_spp, const FrameGeom g) {
+    constexpr bool kInlinePrimary = kInLane && RT_PRIMARY_INLINE;
     extern __shared__ int32_t lds_stack[];
     __shared__ int s_q[kChainSteps], s_sh[kChainSteps];
     for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) { s_q[i] = 0; s_sh[i] = 0; }
@@ -1851,7 +1870,8 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
     if (wt_out && __lane_id() == 0) wt_out[0] = __builtin_amdgcn_s_memrealtime();
     unsigned long long wt_q = 0;
 #endif
-    const int nq = w.counters[first];
+    const int nq = kInlinePrimary ? static_cast<int>(static_cast<int64_t>(g.ntiles) * g.tw * g.th * g.pfx * g.pfy)
+                                  : w.counters[first];
     drive_queries(nq, sc.chain_split & 3, w.wq + (2 * first) * kWqSlot, [&](int j0, int end) {
         const int vb = j0 >> 6;   // this wave's batch in dispatch order (wave-uniform when ordered)
         const int pb = (ordered && (vb << 6) < end) ? w.batch_order[vb] : vb;
@@ -1861,14 +1881,28 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
         [&](int j) {
         if (j >= end) return;
         if (sc.chain_split & 4) j = nq - 1 - j;   // (diagnostic: reversed order)
-        const float4 qo = w.q_org[first & 1][j], qd = w.q_dst[first & 1][j];
-        int lvl = as_int(qd.w);
-        if (lvl < 0) return;
+        V3 org, dst;
+        int lvl, sample;
+        int64_t pxi = -1;
+        if (kInlinePrimary) {   // query j = sample j: its primary ray, as k_gen_primary makes it
+            int sub;
+            if (!primary_sample(g, j, org, dst, pxi, sub)) {
+                if (g.out_mode == 0 && out_u8 && sub == 0) { out_u8[3 * pxi] = 0; out_u8[3 * pxi + 1] = 0; out_u8[3 * pxi + 2] = 0; }
+                return;
+            }
+            lvl = 0;
+            sample = j;
+        } else {
+            const float4 qo = w.q_org[first & 1][j], qd = w.q_dst[first & 1][j];
+            lvl = as_int(qd.w);
+            if (lvl < 0) return;
+            sample = as_int(qo.w);
+            org = mk(qo.x, qo.y, qo.z);
+            dst = mk(qd.x, qd.y, qd.z);
+        }
 #ifdef RT_WAVE_TIMES
         ++wt_q;
 #endif
-        const int sample = as_int(qo.w);
-        V3 org = mk(qo.x, qo.y, qo.z), dst = mk(qd.x, qd.y, qd.z);
         for (int step = first; step < kChainSteps; ++step) {
             if (step > first) atomicAdd(&s_q[step], 1);
             const Secondary sec = chain_step<kAnyHit, W, kCount, kInLane>(sc, p, w, step, sample, org, dst, lvl, stack,
@@ -1883,7 +1917,10 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
             dst = sec.dst;
             lvl = sec.lvl;
         }
-        if (fuse_spp) { if (!kInLane) rgb = fold_chain(w, sample); px = w.pix_out[sample]; }
+        if (fuse_spp) {
+            if (!kInLane) rgb = fold_chain(w, sample);
+            px = kInlinePrimary ? static_cast<int>(pxi) : w.pix_out[sample];
+        }
         }(ordered ? pb * kWave + (j0 & (kWave - 1)) : j0);
         if (fuse_spp) {   // k_frame's arithmetic: a pixel's fuse_spp sub-samples sit in adjacent lanes
             const int lane = __lane_id(), base = lane & ~(fuse_spp - 1);
@@ -2108,12 +2145,15 @@ inline unsigned grid_for(int64_t n) { return static_cast<unsigned>((n + kBlock -
 
 }  // namespace
 
+bool primaries_inline() { return RT_CHAIN_INLANE && RT_PRIMARY_INLINE; }
+
 void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream, bool fused, uint8_t *out_u8) {
     const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th * g.pfx * g.pfy;
     if (n <= 0) return;
     const int64_t clear = std::max<int64_t>(2 * kMaxStepsCounters, 2 * static_cast<int64_t>(w.steps) * kWqSlot);
-    hipLaunchKernelGGL(k_gen_primary, dim3(grid_for(std::max(n, clear))), dim3(kBlock), 0, stream, g, w, out_u8,
-                       fused ? 1 : 0);
+    const bool inl = fused && primaries_inline();   // the chain launch makes the primaries: resets only
+    hipLaunchKernelGGL(k_gen_primary, dim3(grid_for(inl ? clear : std::max(n, clear))), dim3(kBlock), 0, stream, g, w,
+                       out_u8, inl ? 2 : fused ? 1 : 0);
 }
 
 void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevWork &w, hipStream_t stream) {
@@ -2228,14 +2268,14 @@ void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int
 }
 
 void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
-                  hipStream_t stream, bool ordered, uint8_t *out_u8, float *out_f32, int fuse_spp) {
+                  hipStream_t stream, bool ordered, uint8_t *out_u8, float *out_f32, int fuse_spp, const FrameGeom *g) {
     if (capacity <= 0) return;
     const bool wide = tree_variant(s0, -1) == 4;
     const DevScene s = for_width(s0, wide ? 4 : 2);
     auto k = wide ? (s.any_transparent ? k_chain<4, false, false> : k_chain<4, true, false>)
                   : (s.any_transparent ? k_chain<2, false, false> : k_chain<2, true, false>);
     // fused pixel writes from step 0: each lane folds its own chain (RT_CHAIN_INLANE)
-    const bool inlane = RT_CHAIN_INLANE && fuse_spp > 0 && first == 0;
+    const bool inlane = RT_CHAIN_INLANE && fuse_spp > 0 && first == 0 && g != nullptr;
     if (inlane)
         k = wide ? (s.any_transparent ? k_chain<4, false, false, true> : k_chain<4, true, false, true>)
                  : (s.any_transparent ? k_chain<2, false, false, true> : k_chain<2, true, false, true>);
@@ -2247,8 +2287,9 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
         k = wide ? (s.any_transparent ? k_chain<4, false, true> : k_chain<4, true, true>)
                  : (s.any_transparent ? k_chain<2, false, true> : k_chain<2, true, true>);
 #endif
+    const FrameGeom geom = g ? *g : FrameGeom{};
     hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, p, w, first,
-                       s.nodes4, s.leaf_recs, s.leaf_idx, ordered ? 1 : 0, out_u8, out_f32, fuse_spp);
+                       s.nodes4, s.leaf_recs, s.leaf_idx, ordered ? 1 : 0, out_u8, out_f32, fuse_spp, geom);
 }
 
 void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream) {
