@@ -90,6 +90,10 @@ def parse():
     ap.add_argument("--comm", choices=("torch", "rt"), default="torch",
                     help="N>1 gather: torch.distributed (RCCL) + the library's un-permute kernel, or the library's own "
                          "RCCL communicator end to end (rt_render_frames_sharded)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="N>1 rehearsal on ONE GPU: every rank renders on device 0 and the collectives run over "
+                         "gloo with host staging (checks the multi-rank logic where RCCL refuses two ranks per GPU; "
+                         "timings are not scaling numbers)")
     ap.add_argument("--no-cold", action="store_true", help="skip the cold (unordered) first-frame measurement")
     ap.add_argument("--no-path-compare", action="store_true",
                     help="N=1: skip timing the shard path (tiles + un-permute) beside the frame path")
@@ -125,10 +129,25 @@ def main():
     from raytracert_amd import dist as rdist, scenes
     from raytracert_amd._capi import KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME, KERNEL_CHAIN
 
+    if args.rehearse:   # every rank on device 0, gloo collectives on host copies
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+
+    def all_reduce(t, op=None):
+        """dist.all_reduce on a device tensor (host-staged over gloo when rehearsing)."""
+        op = dist.ReduceOp.SUM if op is None else op
+        if not args.rehearse:
+            dist.all_reduce(t, op=op)
+            return
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        t.copy_(h)
 
     wl = WORKLOADS[args.workload]
     WIDTH, HEIGHT, PF, MAX_LVL, LIGHTS = wl["width"], wl["height"], wl["pf"], wl["max_lvl"], wl["lights"]
@@ -158,6 +177,8 @@ def main():
         if rank == 0:
             uid.copy_(torch.frombuffer(bytearray(R.Comm.unique_id()), dtype=torch.uint8))
         if world > 1:
+            if args.rehearse:
+                raise SystemExit("--comm rt needs one GPU per rank (RCCL refuses two ranks on one device)")
             dist.broadcast(uid, 0)
         rtcomm = R.Comm(local_rank, rank, world, bytes(uid.cpu().numpy().tobytes()))
 
@@ -222,7 +243,14 @@ def main():
                                             out.numel() if rank == 0 else 0, stream.cuda_stream)
                 return out.view(self.plan.frames, HEIGHT, WIDTH, 3) if rank == 0 else None
             self.render_shard(buf=self.bufs[i % 2])
-            self.pending.append(rdist.gather_shards(self.bufs[i % 2], rank, world, async_op=True))
+            if args.rehearse and world > 1:   # host-staged gather over gloo (synchronous)
+                torch.cuda.synchronize(dev)
+                h = self.bufs[i % 2].cpu()
+                parts = [torch.empty_like(h) for _ in range(world)] if rank == 0 else None
+                dist.gather(h, parts, dst=0)
+                self.pending.append((torch.cat(parts).to(dev) if rank == 0 else None, None))
+            else:
+                self.pending.append(rdist.gather_shards(self.bufs[i % 2], rank, world, async_op=True))
             return self.finish(self.pending.pop(0)) if len(self.pending) > 1 else None
 
         def drain(self):
@@ -250,7 +278,7 @@ def main():
                 dist.barrier()
             el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
             if world > 1:
-                dist.all_reduce(el, op=dist.ReduceOp.MAX)
+                all_reduce(el, dist.ReduceOp.MAX)
             return float(el.item()), frames
 
     main_run = Runner(world if args.mode == "weak" else 1, frame_path=world == 1 and rtcomm is None)
@@ -260,12 +288,22 @@ def main():
     counts = main_run.render_shard(want_counts=True)
     ct = torch.tensor([int(c) for c in counts], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(ct)
+        all_reduce(ct)
     rays_per_step = float(ct.sum().item())
     rays_by_kind = [int(x) for x in ct.tolist()]
 
     # ---- timed region (the metric) ----
     elapsed, frames = main_run.run(args.steps, args.warmup)
+
+    rehearsal = None
+    if args.rehearse and rank == 0 and frames is not None:   # every assembled frame = the one-GPU frame
+        fb = torch.zeros(HEIGHT * WIDTH * 3, dtype=torch.uint8, device=dev)
+        scene.render_frame_device(cparams, TILE, TILE, fb.data_ptr(), fb.numel(), stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        ref = fb.view(HEIGHT, WIDTH, 3)
+        rehearsal = {"frames_checked": int(frames.shape[0]),
+                     "all_equal_one_gpu_frame": bool(all(torch.equal(frames[f], ref) for f in range(frames.shape[0]))),
+                     "note": "ranks share one GPU; gloo host-staged gather: logic check, not a scaling number"}
 
     # ---- a cold frame: no measured batch order yet (the first frame of a new view) ----
     scene.tune("batch_order", 0)   # screen-order dispatch, exactly what a view's first launch does
@@ -405,6 +443,8 @@ def main():
                 "parallelism": f"tile-shard{world}",
                 "path": ("rt_render_frame_device" if main_run.single else
                          "rt_render_frames_sharded (library RCCL gather + un-permute)" if rtcomm is not None else
+                         "rt_render_tiles_device + gloo host-staged gather (rehearsal) + rt_assemble_tiles_device"
+                         if args.rehearse else
                          "rt_render_tiles_device + RCCL gather (torch.distributed) + rt_assemble_tiles_device"),
                 "rays_per_step": int(rays_per_step),
                 "rays_by_kind_per_step": {"primary": rays_by_kind[0], "secondary": rays_by_kind[1], "shadow": rays_by_kind[2]},
@@ -450,6 +490,8 @@ def main():
             "cpu_baseline": None,
         }
         result.update(extra)
+        if rehearsal is not None:
+            result["rehearsal"] = rehearsal
         if args.ppm and frames is not None:
             R.write_ppm(args.ppm, frames[0].cpu().numpy())
 
