@@ -112,3 +112,21 @@ def test_render_frames_sharded_two_processes(workdir, tmp_path, gpu_available):
         full, _ = _frame(sc, p)
     got = np.load(out).reshape(2, 70, 100, 3)
     assert np.array_equal(got[0], full) and np.array_equal(got[1], full)
+
+
+def test_bench_multi_rank_rehearsal(tmp_path, gpu_available):
+    """bench.py's N>1 step (interleaved tiles per rank, one gather to rank 0, the library's
+    un-permute, max-over-ranks timing, the strong-scaling re-run) with two ranks sharing the one
+    GPU over gloo (--rehearse): every assembled frame equals the one-GPU frame."""
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", "29533", os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--rehearse", "--workload", "c2", "--no-cpu", "--no-bf-roofline", "--no-cold",
+           "--no-path-compare"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 2 and d["config"]["frames_per_step"] == 2
+    assert d["rehearsal"]["frames_checked"] == 2 and d["rehearsal"]["all_equal_one_gpu_frame"]
+    assert d["config"]["rays_per_step"] == 2 * 494405 and "strong" in d
