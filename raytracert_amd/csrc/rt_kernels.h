@@ -6,6 +6,7 @@
 
 #include <cstdint>
 
+#include "fastdiv.h"
 #include "rt_internal.h"
 
 namespace rt {
@@ -26,6 +27,8 @@ struct FrameGeom {
     int32_t stochastic;                 // RT_STOCHASTIC: jittered sub-samples
     uint32_t seed;                      // its hash seed
     float corners[8][3];                // origin00,dest00,origin01,dest01,origin10,dest10,origin11,dest11
+    // divisions by the geometry, as multiply-high + shifts (fastdiv.h); the launchers fill them
+    UDiv div_spp, div_tpx, div_tiles, div_tx, div_tw, div_pfy;
 };
 
 struct ShadeParams {

@@ -1386,14 +1386,17 @@ __global__ __launch_bounds__(kBlock) void k_intersect_only(const TriRec *__restr
 // ---------------------------------------------------------------------------------------------
 // Sample generation: main.cpp:377-386 for every sub-sample of the batch's tiles.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ bool decode_pixel(const FrameGeom &g, int64_t pix, int &x, int &y) {
-    const int tpx = g.tw * g.th;
-    const int tl = static_cast<int>(pix / tpx);
-    const int p = static_cast<int>(pix - static_cast<int64_t>(tl) * tpx);
-    const int tid = (g.first + (g.tile0 + tl) * g.stride) % g.tiles_total;
-    const int tx = tid % g.tiles_x, ty = tid / g.tiles_x;
-    x = g.ox + tx * g.tw + (p % g.tw);
-    y = g.oy + ty * g.th + (p / g.tw);
+// (Indices are below 2^31: batches are capped at 2^30 samples and tile ids at 2^30, rt_capi.cpp.)
+__device__ __forceinline__ bool decode_pixel(const FrameGeom &g, int64_t pix64, int &x, int &y) {
+    const uint32_t pix = static_cast<uint32_t>(pix64);
+    const uint32_t tl = udiv(pix, g.div_tpx);
+    const uint32_t p = pix - tl * g.div_tpx.d;
+    const uint32_t tid = umod(static_cast<uint32_t>(g.first) + (static_cast<uint32_t>(g.tile0) + tl) * static_cast<uint32_t>(g.stride),
+                              g.div_tiles);
+    const uint32_t ty = udiv(tid, g.div_tx), tx = tid - ty * g.div_tx.d;
+    const uint32_t py = udiv(p, g.div_tw), pxl = p - py * g.div_tw.d;
+    x = g.ox + static_cast<int>(tx) * g.tw + static_cast<int>(pxl);
+    y = g.oy + static_cast<int>(ty) * g.th + static_cast<int>(py);
     return x < g.width && y < g.height && x < g.ox + g.cw && y < g.oy + g.ch && x >= 0 && y >= 0;
 }
 
@@ -1410,9 +1413,10 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
 // samples outside the frame or the clip rectangle (origin and dest then (0,0,0)).
 __device__ __forceinline__ bool primary_sample(const FrameGeom &g, int64_t s, V3 &origin, V3 &dest, int64_t &px, int &sub) {
     const int spp = g.pfx * g.pfy;
-    const int64_t pix = s / spp;
+    const int64_t pix = udiv(static_cast<uint32_t>(s), g.div_spp);
     sub = static_cast<int>(s - pix * spp);
-    const int subx = sub / g.pfy, suby = sub - subx * g.pfy;   // subx outer, suby inner (:377-378)
+    const int subx = static_cast<int>(udiv(static_cast<uint32_t>(sub), g.div_pfy));
+    const int suby = sub - subx * g.pfy;   // subx outer, suby inner (:377-378)
     int x, y;
     const bool valid = decode_pixel(g, pix, x, y);
     px = g.out_mode == 0 ? static_cast<int64_t>(g.tile0) * g.tw * g.th + pix
@@ -2147,13 +2151,24 @@ inline unsigned grid_for(int64_t n) { return static_cast<unsigned>((n + kBlock -
 
 bool primaries_inline() { return RT_CHAIN_INLANE && RT_PRIMARY_INLINE; }
 
+// The geometry's divisors as multiply-high magic numbers (fastdiv.h), for the kernels' index decoding.
+static FrameGeom with_divisors(FrameGeom g) {
+    g.div_spp = make_udiv(static_cast<uint32_t>(g.pfx * g.pfy));
+    g.div_tpx = make_udiv(static_cast<uint32_t>(g.tw * g.th));
+    g.div_tiles = make_udiv(static_cast<uint32_t>(std::max(g.tiles_total, 1)));
+    g.div_tx = make_udiv(static_cast<uint32_t>(std::max(g.tiles_x, 1)));
+    g.div_tw = make_udiv(static_cast<uint32_t>(g.tw));
+    g.div_pfy = make_udiv(static_cast<uint32_t>(g.pfy));
+    return g;
+}
+
 void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream, bool fused, uint8_t *out_u8) {
     const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th * g.pfx * g.pfy;
     if (n <= 0) return;
     const int64_t clear = std::max<int64_t>(2 * kMaxStepsCounters, 2 * static_cast<int64_t>(w.steps) * kWqSlot);
     const bool inl = fused && primaries_inline();   // the chain launch makes the primaries: resets only
-    hipLaunchKernelGGL(k_gen_primary, dim3(grid_for(inl ? clear : std::max(n, clear))), dim3(kBlock), 0, stream, g, w,
-                       out_u8, inl ? 2 : fused ? 1 : 0);
+    hipLaunchKernelGGL(k_gen_primary, dim3(grid_for(inl ? clear : std::max(n, clear))), dim3(kBlock), 0, stream,
+                       with_divisors(g), w, out_u8, inl ? 2 : fused ? 1 : 0);
 }
 
 void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevWork &w, hipStream_t stream) {
@@ -2287,7 +2302,7 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
         k = wide ? (s.any_transparent ? k_chain<4, false, true> : k_chain<4, true, true>)
                  : (s.any_transparent ? k_chain<2, false, true> : k_chain<2, true, true>);
 #endif
-    const FrameGeom geom = g ? *g : FrameGeom{};
+    const FrameGeom geom = g ? with_divisors(*g) : FrameGeom{};
     hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, p, w, first,
                        s.nodes4, s.leaf_recs, s.leaf_idx, ordered ? 1 : 0, out_u8, out_f32, fuse_spp, geom);
 }
@@ -2295,7 +2310,7 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
 void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream) {
     const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th;
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_frame, dim3(grid_for(n)), dim3(kBlock), 0, stream, g, w, out_u8, out_f32);
+    hipLaunchKernelGGL(k_frame, dim3(grid_for(n)), dim3(kBlock), 0, stream, with_divisors(g), w, out_u8, out_f32);
 }
 
 void launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream, bool xcd_segments) {
