@@ -624,11 +624,33 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
 #endif
 constexpr int32_t kDoneRef = kBvhEmpty;   // "no ref": a count-0 leaf is never a wanted child
 
+#ifndef RT_NODE_V2
+#define RT_NODE_V2 1   // per-ray slab offsets folded into one FMA per plane; exponent by v_ldexp_f32
+#endif
+#ifndef RT_FAST_SETUP
+#define RT_FAST_SETUP 1   // approximate reciprocals in the per-ray traversal constants (conservative margins)
+#endif
+
+// Per-ray traversal constants. With RT_NODE_V2 a child's slab plane is
+//   t = fma(q, 2^e * inv, fma(origin, inv, (-/+pad - o) * inv))
+// instead of fma(q, 2^e * inv, (origin - o -/+ pad) * inv): the same value up to a few ulps of
+// (|o| + pad) * |inv| and of |t|, inside the pad (64 ulps of |o| + the scene's extent) and the
+// 1e-5 relative slack of the te <= tx test.
 struct Ray4 {
     V3 o, inv;
     float pnx, pny, pnz, tcull;
+    float bnx, bny, bnz, bfx, bfy, bfz;   // RT_NODE_V2: (+/-pad - o) * inv per axis, near and far plane
+    float inv_dlen;                       // RT_FAST_SETUP: an upper bound of 1.00001 / |dir|
     bool nx, ny, nz;
 };
+
+// tcull for the current best: no child whose entry parameter exceeds it can hold a hit at
+// distance <= best (bvh4_query). RT_FAST_SETUP multiplies by a reciprocal rounded up by 1e-4,
+// which only raises tcull (visits no fewer nodes than the division form).
+__device__ __forceinline__ float cull_param(const Ray4 &R, float best, float pad, float dlen) {
+    if (RT_FAST_SETUP) return (best * 1.00002f + pad) * R.inv_dlen;
+    return (best * 1.00002f + pad) / dlen * 1.00001f;
+}
 
 // One node visit: the wanted children by entry distance, the far ones pushed; returns the next ref
 // (the nearest wanted child, else the stack top, else kDoneRef).
@@ -636,13 +658,25 @@ template <bool kAnyHit>
 __device__ __forceinline__ int32_t node4_next(const Ray4 &R, uint4 a, uint4 b, uint4 c, uint4 d, const LaneStack &stack,
                                               int &sp) {
     const V3 o = R.o, inv = R.inv;
-    const float dx = __uint_as_float(a.x) - o.x, dy = __uint_as_float(a.y) - o.y, dz = __uint_as_float(a.z) - o.z;
-    const float kx = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w)) + 127) << 23) * inv.x;
-    const float ky = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 8)) + 127) << 23) * inv.y;
-    const float kz = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 16)) + 127) << 23) * inv.z;
-    const float cnx = (dx + R.pnx) * inv.x, cfx = (dx - R.pnx) * inv.x;
-    const float cny = (dy + R.pny) * inv.y, cfy = (dy - R.pny) * inv.y;
-    const float cnz = (dz + R.pnz) * inv.z, cfz = (dz - R.pnz) * inv.z;
+    float kx, ky, kz, cnx, cfx, cny, cfy, cnz, cfz;
+    if (RT_NODE_V2) {
+        // 2^e * inv is exact (or the same overflow) either way; v_ldexp_f32 takes the int8 exponent
+        kx = __builtin_amdgcn_ldexpf(inv.x, static_cast<int>(static_cast<int8_t>(a.w)));
+        ky = __builtin_amdgcn_ldexpf(inv.y, static_cast<int>(static_cast<int8_t>(a.w >> 8)));
+        kz = __builtin_amdgcn_ldexpf(inv.z, static_cast<int>(static_cast<int8_t>(a.w >> 16)));
+        const float ox = __uint_as_float(a.x), oy = __uint_as_float(a.y), oz = __uint_as_float(a.z);
+        cnx = fmaf(ox, inv.x, R.bnx); cfx = fmaf(ox, inv.x, R.bfx);
+        cny = fmaf(oy, inv.y, R.bny); cfy = fmaf(oy, inv.y, R.bfy);
+        cnz = fmaf(oz, inv.z, R.bnz); cfz = fmaf(oz, inv.z, R.bfz);
+    } else {
+        const float dx = __uint_as_float(a.x) - o.x, dy = __uint_as_float(a.y) - o.y, dz = __uint_as_float(a.z) - o.z;
+        kx = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w)) + 127) << 23) * inv.x;
+        ky = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 8)) + 127) << 23) * inv.y;
+        kz = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 16)) + 127) << 23) * inv.z;
+        cnx = (dx + R.pnx) * inv.x; cfx = (dx - R.pnx) * inv.x;
+        cny = (dy + R.pny) * inv.y; cfy = (dy - R.pny) * inv.y;
+        cnz = (dz + R.pnz) * inv.z; cfz = (dz - R.pnz) * inv.z;
+    }
     const uint32_t wnx = R.nx ? b.w : b.x, wfx = R.nx ? b.x : b.w;
     const uint32_t wny = R.ny ? c.x : b.y, wfy = R.ny ? b.y : c.x;
     const uint32_t wnz = R.nz ? c.y : b.z, wfz = R.nz ? b.z : c.y;
@@ -658,7 +692,8 @@ __device__ __forceinline__ int32_t node4_next(const Ray4 &R, uint4 a, uint4 b, u
         const float tx = fminf(fminf(tfx, tfy), tfz);
         bool h = te <= tx * 1.00001f;
         if (!kAnyHit) h = h && te <= R.tcull;
-        tc[k] = h ? fminf(te, FLT_MAX) : INFINITY;
+        // te >= 0 (or NaN, then h is false): an integer min keeps a hit child's key below INFINITY
+        tc[k] = h ? __uint_as_float(min(__float_as_uint(te), 0x7f7fffffu)) : INFINITY;
     }
     if (RT_NODE_BRANCHFREE && (!kAnyHit || RT_NODE_BRANCHFREE > 1)) {
         // Branch-free pushes: the wanted children after the first go to the stack with
@@ -736,17 +771,26 @@ __device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, 
     test_always<kAnyHit>(sc, o, dir, best, bidx, bI, done);
     if (!active || (kAnyHit && done)) return;
     Ray4 R;   // bvh4_query's per-ray constants
-    V3 inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+    // RT_FAST_SETUP: v_rcp_f32 (1 ulp) for the slab reciprocals; every plane of every node uses the
+    // same inv, and a 1-ulp change of one axis' scale moves its slab parameters by 2^-23 relative,
+    // inside the 1e-5 slack of the te <= tx test and the tcull bound.
+    V3 inv = RT_FAST_SETUP ? mk(__builtin_amdgcn_rcpf(dir.x), __builtin_amdgcn_rcpf(dir.y), __builtin_amdgcn_rcpf(dir.z))
+                           : mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
     constexpr float kInvMax = 0x1p100f;
     if (!(fabsf(inv.x) <= kInvMax)) inv.x = copysignf(kInvMax, dir.x);
     if (!(fabsf(inv.y) <= kInvMax)) inv.y = copysignf(kInvMax, dir.y);
     if (!(fabsf(inv.z) <= kInvMax)) inv.z = copysignf(kInvMax, dir.z);
     const float pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
-    const float dlen = sqrtf(dot(dir, dir));
+    const float dlen2 = dot(dir, dir);
+    const float dlen = RT_FAST_SETUP ? 0.0f : sqrtf(dlen2);
+    // 1.00001 / |dir| with v_rsq_f32 (1 ulp) rounded up by 1e-4: never below the division form
+    R.inv_dlen = RT_FAST_SETUP ? __builtin_amdgcn_rsqf(dlen2) * 1.00011f : 0.0f;
     R.o = o;
     R.inv = inv;
     R.nx = inv.x < 0; R.ny = inv.y < 0; R.nz = inv.z < 0;
     R.pnx = R.nx ? pad : -pad; R.pny = R.ny ? pad : -pad; R.pnz = R.nz ? pad : -pad;
+    R.bnx = (R.pnx - o.x) * inv.x; R.bny = (R.pny - o.y) * inv.y; R.bnz = (R.pnz - o.z) * inv.z;
+    R.bfx = (-R.pnx - o.x) * inv.x; R.bfy = (-R.pny - o.y) * inv.y; R.bfz = (-R.pnz - o.z) * inv.z;
     R.tcull = INFINITY;
     int sp = 0;
     int32_t node = 0;          // inner node to visit, a leaf ref, or kDoneRef
@@ -791,7 +835,7 @@ __device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, 
                 tests += static_cast<unsigned>(cnt);
                 if (kAnyHit && done) { node = kDoneRef; leaf2 = kDoneRef; break; }
             }
-            if (!kAnyHit && best < FLT_MAX) R.tcull = (best * 1.00002f + pad) / dlen * 1.00001f;
+            if (!kAnyHit && best < FLT_MAX) R.tcull = cull_param(R, best, pad, dlen);
             leaf = kDoneRef;
             if (RT_WW_LEAVES > 1 && leaf2 != kDoneRef) {
                 leaf = leaf2;
