@@ -270,6 +270,13 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
 #define RT_TUNE_FUSE_PIXELS 18  /* 1 (default): the chain launch writes each pixel when its samples'
                                     chains end (no separate frame pass) when pf*pf divides 64;
                                     0: always the frame pass */
+#define RT_TUNE_CHAIN_REFILL 19  /* 1: in the chain launch each lane owns one pixel at a time, runs its
+                                    sub-samples' chains in order and then takes the next pixel (per-XCD
+                                    work counters), so lanes do not wait for a batch's longest chain;
+                                    0 (default): fixed 64-sample batches with the batch order (measured
+                                    faster: a wave's rays then share a chain step and stay coherent) */
+#define RT_TUNE_REFILL_GRID 20   /* blocks (of 128 threads) of the refill chain launch (default: resident,
+                                    10 per CU) */
 #define RT_TUNE_TOP_NODES 13     /* four-wide nodes of the tree's top levels (breadth-first, the first
                                     ones in the node array) each block reads from an LDS copy (0-85) */
 #define RT_TUNE_CHAIN_SPLIT 12   /* query distribution of the chain launch: as RT_TUNE_XCD_SPLIT, or 3: 64-query

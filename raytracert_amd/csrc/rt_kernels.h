@@ -86,6 +86,8 @@ struct DevScene {
     unsigned long long *work;       // BVH kernels' work counters: [0, kWorkFields) closest-hit, then shadow
     int32_t chain_split;            // RT_TUNE_CHAIN_SPLIT: query distribution of k_chain (as xcd_split)
     int32_t top_nodes;              // RT_TUNE_TOP_NODES: four-wide nodes [0, top_nodes) read from an LDS copy
+    int32_t chain_refill;           // RT_TUNE_CHAIN_REFILL: per-lane pixel refill in the chain launch
+    int32_t refill_grid;            // its (resident) grid, blocks of 128 threads
 };
 
 struct DevWork {
@@ -132,6 +134,10 @@ void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *
 // k_frame's arithmetic, so no k_frame follows.
 // g (fused launches from step 0): the batch's frame geometry; in-lane chain kernels then make their
 // primary rays themselves (launch_gen_primary(fused) only resets the counters; primaries_inline()).
+// blocks of 128 threads of the chain kernels resident per CU (4 SIMDs x waves per EU / 2)
+int chain_blocks_per_cu();
+// whether launch_chain runs the per-lane refill kernel (k_chain_refill) for these arguments
+bool chain_refill_used(const DevScene &s, int fuse_spp, const FrameGeom *g);
 void launch_chain(const DevScene &s, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
                   hipStream_t stream, bool ordered = false, uint8_t *out_u8 = nullptr, float *out_f32 = nullptr,
                   int fuse_spp = 0, const FrameGeom *g = nullptr);

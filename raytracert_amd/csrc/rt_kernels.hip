@@ -2001,6 +2001,127 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Chain launch with per-lane refill (RT_TUNE_CHAIN_REFILL 1; measured 1.5x slower than k_chain on C4
+// and 1.3x on C2, so not the default: mixing chain steps in a wave breaks the coherence of the
+// rays that k_chain's lanes trace side by side): a lane owns one pixel at a
+// time and runs its sub-samples' chains one after the other (main.cpp:377-391, summed in the same
+// order as k_frame); when the pixel is written it takes the next pixel from the wave's pool, which
+// the wave fills 64 pixels at a time from per-XCD work counters. Lanes no longer idle behind the
+// longest chain of a fixed 64-sample batch (k_chain: ~44% VALU lane utilisation on C4), and the
+// launch's tail is one pixel's chains rather than one batch's. Each step is chain_step, the same
+// arithmetic and record layout as k_chain, so results are identical; only placement changes.
+// ---------------------------------------------------------------------------------------------
+constexpr int kRefillChunk = 64;   // pixels per work-counter take (>= a wave's lanes)
+
+template <int W, bool kAnyHit, bool kCount>
+__global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CHAIN_WPE))) void k_chain_refill(
+    const DevScene sc, const ShadeParams p, DevWork w, const Bvh4Node *__restrict__ n4,
+    const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx, uint8_t *__restrict__ out_u8,
+    float *__restrict__ out_f32, const FrameGeom g) {
+    extern __shared__ int32_t lds_stack[];
+    __shared__ int s_q[kChainSteps], s_sh[kChainSteps];
+    for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) { s_q[i] = 0; s_sh[i] = 0; }
+    __syncthreads();
+    const LaneStack stack = lane_stack(sc, lds_stack);
+    WorkTally<kCount> wc, ws;
+    const int spp = g.pfx * g.pfy;
+    const int npix = g.ntiles * g.tw * g.th;
+    const int lane = __lane_id();
+    const int home = blockIdx.x % kXcds;
+    int32_t *__restrict__ wq = w.wq;   // the step-0 chain slot: one counter per XCD (reset by k_gen_primary)
+    int pool = 0, pool_end = 0, xk = 0;   // wave-uniform: pixels [pool, pool_end) not handed out; counters tried
+    int pix = -1, sub = 0, step = 0, lvl = 0, sample = 0;
+    int64_t pxo = -1;
+    V3 acc = mk(0, 0, 0), org = mk(0, 0, 0), dst = mk(0, 0, 0);
+    // sample pix * spp + sub of this lane's pixel: its primary ray (false: outside the frame)
+    auto begin_sample = [&]() -> bool {
+        sample = pix * spp + sub;
+        int sub_out;
+        if (!primary_sample(g, sample, org, dst, pxo, sub_out)) return false;
+        step = 0;
+        lvl = 0;
+        return true;
+    };
+    while (true) {
+        // hand a pixel to every lane without one
+        const uint64_t idle = __ballot(pix < 0);
+        if (idle) {
+            const int nidle = __popcll(idle);
+            const int rank = __popcll(idle & ((1ull << lane) - 1ull));
+            const int avail = pool_end - pool;
+            int fresh = -1, fresh_len = 0;
+            while (avail < nidle && xk < kXcds) {   // take another chunk (own XCD first, then the others)
+                const int gx = (home + xk) % kXcds;
+                int c = 0;
+                if (lane == 0) c = atomicAdd(&wq[gx * kWqStride], 1);
+                c = __shfl(c, 0);
+                const int64_t start = (static_cast<int64_t>(c) * kXcds + gx) * kRefillChunk;
+                if (start < npix) {
+                    fresh = static_cast<int>(start);
+                    fresh_len = min(kRefillChunk, npix - fresh);
+                    break;
+                }
+                ++xk;
+            }
+            if (pix < 0) {
+                if (rank < avail) pix = pool + rank;
+                else if (rank - avail < fresh_len) pix = fresh + (rank - avail);
+            }
+            if (fresh >= 0) {
+                const int used = min(nidle - avail, fresh_len);
+                pool = fresh + used;
+                pool_end = fresh + fresh_len;
+            } else {
+                pool += min(nidle, avail);
+            }
+            if ((idle >> lane) & 1ull) {
+                if (pix >= 0) {
+                    sub = 0;
+                    acc = mk(0, 0, 0);
+                    if (!begin_sample()) {   // outside the frame: black in the tile-major layout (k_frame)
+                        if (g.out_mode == 0 && out_u8) { out_u8[3 * pxo] = 0; out_u8[3 * pxo + 1] = 0; out_u8[3 * pxo + 2] = 0; }
+                        pix = -1;
+                    }
+                }
+            }
+        }
+        if (!__ballot(pix >= 0)) {
+            if (xk >= kXcds && pool >= pool_end) break;   // every counter is spent and no lane has work
+            continue;
+        }
+        if (pix >= 0) {
+            if (step > 0) atomicAdd(&s_q[step], 1);
+            const Secondary sec = chain_step<kAnyHit, W, kCount, true>(sc, p, w, step, sample, org, dst, lvl, stack,
+                                                                      lds_stack, n4, lrec, lidx, s_sh, wc, ws);
+            if (sec.state != kChildTrace) {   // the chain ends: fold it (fold_chain's arithmetic)
+                const V3 rgb = fold_inlane(sc, w, 0, step, sample,
+                                           sec.state == kChildZero ? add(sec.local, mk(0.0f, 0.0f, 0.0f)) : sec.local);
+                acc = add(acc, rgb);   // sub-samples in order, from (0, 0, 0) (k_frame)
+                if (++sub == spp) {
+                    const float div = static_cast<float>(spp);
+                    store_pixel(mk(acc.x / div, acc.y / div, acc.z / div), 3 * pxo, out_u8, out_f32);   // operator/
+                    pix = -1;
+                } else {
+                    begin_sample();   // (same pixel: inside the frame)
+                }
+            } else {
+                org = sec.org;
+                dst = sec.dst;
+                lvl = sec.lvl;
+                ++step;
+            }
+        }
+    }
+    wc.flush(sc.work);
+    ws.flush(sc.work ? sc.work + kWorkFields : nullptr);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) {
+        if (s_q[i]) atomicAdd(&w.counters[i], s_q[i]);
+        if (s_sh[i]) atomicAdd(&w.counters[kMaxStepsCounters + i], s_sh[i]);
+    }
+}
+
 // Frame: per pixel, sum sub-samples (subx outer, suby inner), divide by pf^2 (main.cpp:391),
 // clamp (RGBValue, main.cpp:29-41), quantise with truncation (main.cpp:117; NaN -> 0).
 __global__ __launch_bounds__(kBlock) void k_frame(const FrameGeom g, DevWork w, uint8_t *__restrict__ out_u8,
@@ -2347,8 +2468,27 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
                  : (s.any_transparent ? k_chain<2, false, true> : k_chain<2, true, true>);
 #endif
     const FrameGeom geom = g ? with_divisors(*g) : FrameGeom{};
+    if (inlane && chain_refill_used(s0, fuse_spp, g)) {
+        auto kr = wide ? (s.any_transparent ? k_chain_refill<4, false, false> : k_chain_refill<4, true, false>)
+                       : (s.any_transparent ? k_chain_refill<2, false, false> : k_chain_refill<2, true, false>);
+        if (s.work)
+            kr = wide ? (s.any_transparent ? k_chain_refill<4, false, true> : k_chain_refill<4, true, true>)
+                      : (s.any_transparent ? k_chain_refill<2, false, true> : k_chain_refill<2, true, true>);
+        // a resident grid: every wave keeps taking pixels until the counters are spent
+        const unsigned grid = std::min<unsigned>(grid_bvh(capacity, s.bvh_grid), static_cast<unsigned>(s.refill_grid));
+        hipLaunchKernelGGL(kr, dim3(grid), dim3(kBvhBlock), bvh_lds(s), stream, s, p, w, s.nodes4, s.leaf_recs,
+                           s.leaf_idx, out_u8, out_f32, geom);
+        return;
+    }
     hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, p, w, first,
                        s.nodes4, s.leaf_recs, s.leaf_idx, ordered ? 1 : 0, out_u8, out_f32, fuse_spp, geom);
+}
+
+int chain_blocks_per_cu() { return 4 * RT_CHAIN_WPE * kWave / kBvhBlock; }
+
+bool chain_refill_used(const DevScene &s, int fuse_spp, const FrameGeom *g) {
+    return RT_CHAIN_INLANE && primaries_inline() && s.chain_refill && s.refill_grid > 0 && fuse_spp > 0 && g != nullptr &&
+           s.use_bvh;
 }
 
 void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream) {

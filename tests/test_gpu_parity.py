@@ -380,7 +380,10 @@ def test_multi_frame_shard_batch_reassembles(workdir, gpu_available):
                                    {"chain_from": 1, "bvh_width": 2}, {"chain_from": 0, "pipes": 1},
                                    {"pipes": 2}, {"pipes": 2, "bvh_grid": 4096}, {"bvh_grid": 65536},
                                    {"fuse_pixels": 0}, {"batch_order": 2}, {"batch_order": 2, "chain_split": 3},
-                                   {"chain_split": 1}, {"chain_split": 2}])
+                                   {"chain_split": 1}, {"chain_split": 2}, {"chain_refill": 1},
+                                   {"chain_refill": 1, "batch_order": 0}, {"chain_refill": 1, "refill_grid": 1},
+                                   {"chain_refill": 1, "refill_grid": 3}, {"chain_refill": 1, "refill_grid": 7, "lds_stack": 1},
+                                   {"chain_refill": 1, "refill_grid": 5, "bvh_width": 2}])
 def test_launch_shape_knobs_never_change_results(knobs, workdir, gpu_available):
     """Query distribution (grid-stride, static XCD segments, work-stealing XCD queues), tiny grids
     (fewer blocks than XCDs), tree width and the LDS/HBM split of the traversal stack (1 entry in
@@ -395,6 +398,28 @@ def test_launch_shape_knobs_never_change_results(knobs, workdir, gpu_available):
         u8, f32, c = sc.render(p, want_f32=True)
     assert [int(x) for x in c] == [int(x) for x in refc]
     assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
+
+
+@pytest.mark.parametrize("spec,w,h,pf,flags", [("syn:C4", 333, 187, 1, 0), ("syn:C4", 160, 90, 2, 0),
+                                               ("syn:F4", 96, 54, 3, 0), ("ref:dodgeColorTest.obj", 200, 150, 1, 0),
+                                               ("syn:F3", 70, 41, 2, 1 << 8), ("syn:F4", 17, 9, 1, 0)])
+def test_chain_refill_matches_fixed_batches(spec, w, h, pf, flags, workdir, gpu_available):
+    """RT_TUNE_CHAIN_REFILL 1: lanes take a new pixel when their pixel's chains end, so
+    chains of different samples and steps share a wave; every chain still runs chain_step on its own
+    sample, so frames (bytes and floats), ray counts and the tile-major device output equal the
+    fixed-batch launch's, with transparency (closest-hit shadows), pf 1-3 and jittered sampling."""
+    p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]],
+                       flags=R.ALL_FEATURES | flags, seed=7)
+    with R.Scene.load(scene_path(spec, workdir), device=0) as sc:
+        sc.tune("chain_refill", 0)
+        ref, reff, refc = sc.render(p, want_f32=True)
+        sc.tune("chain_refill", 1)
+        for grid in (0, 2):
+            if grid:
+                sc.tune("refill_grid", grid)
+            u8, f32, c = sc.render(p, want_f32=True)
+            assert [int(x) for x in c] == [int(x) for x in refc]
+            assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
 
 
 @pytest.mark.parametrize("spec,w,h,pf", [("syn:F3", 128, 72, 2), ("syn:F4", 96, 54, 2), ("ref:dodgeColorTest.obj", 80, 60, 3)])
