@@ -268,7 +268,8 @@ class Scene:
              "chain_split": _capi.TUNE_CHAIN_SPLIT, "top_nodes": _capi.TUNE_TOP_NODES,
              "batch_order": _capi.TUNE_BATCH_ORDER,
              "order_every": _capi.TUNE_ORDER_EVERY, "fuse_pixels": _capi.TUNE_FUSE_PIXELS,
-             "chain_refill": _capi.TUNE_CHAIN_REFILL, "refill_grid": _capi.TUNE_REFILL_GRID}[knob]
+             "chain_refill": _capi.TUNE_CHAIN_REFILL, "refill_grid": _capi.TUNE_REFILL_GRID,
+             "wave_steal": _capi.TUNE_WAVE_STEAL}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
 
     def bvh_digest(self) -> int:

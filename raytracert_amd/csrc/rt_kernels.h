@@ -87,6 +87,7 @@ struct DevScene {
     int32_t chain_split;            // RT_TUNE_CHAIN_SPLIT: query distribution of k_chain (as xcd_split)
     int32_t top_nodes;              // RT_TUNE_TOP_NODES: four-wide nodes [0, top_nodes) read from an LDS copy
     int32_t chain_refill;           // RT_TUNE_CHAIN_REFILL: per-lane pixel refill in the chain launch
+    int32_t wave_steal;             // RT_TUNE_WAVE_STEAL: 0 off, 1 on, 2 when the chain launch is <= 2 wave rounds
     int32_t refill_grid;            // its (resident) grid, blocks of 128 threads
 };
 

@@ -231,6 +231,11 @@ struct LaneStack {
         else ovf[static_cast<size_t>(sp - cap) * stride + gl] = v;
         ++sp;
     }
+    __device__ __forceinline__ int32_t at(int k) const {   // entry k of this lane's stack
+        int32_t v = lds[min(k, cap - 1) * width + static_cast<int>(threadIdx.x)];
+        if (k >= cap) v = ovf[static_cast<size_t>(k - cap) * stride + gl];
+        return v;
+    }
     __device__ __forceinline__ int32_t pop(int &sp) const {
         --sp;
         // the LDS read is unconditional so the two reads stay a ds_read and a global load (a
@@ -656,7 +661,7 @@ __device__ __forceinline__ float cull_param(const Ray4 &R, float best, float pad
 // (the nearest wanted child, else the stack top, else kDoneRef).
 template <bool kAnyHit>
 __device__ __forceinline__ int32_t node4_next(const Ray4 &R, uint4 a, uint4 b, uint4 c, uint4 d, const LaneStack &stack,
-                                              int &sp) {
+                                              int &sp, int base = 0) {   // entries [base, sp) are this walk's
     const V3 o = R.o, inv = R.inv;
     float kx, ky, kz, cnx, cfx, cny, cfy, cnz, cfz;
     if (RT_NODE_V2) {
@@ -723,11 +728,11 @@ __device__ __forceinline__ int32_t node4_next(const Ray4 &R, uint4 a, uint4 b, u
         if (nh > 0) return rc[0];
         if (__all(sp <= stack.cap)) {
             const int32_t top = stack.lds[max(sp - 1, 0) * stack.width + lane];
-            const int32_t r = sp > 0 ? top : kDoneRef;
-            sp = max(sp - 1, 0);
+            const int32_t r = sp > base ? top : kDoneRef;
+            sp = max(sp - 1, base);
             return r;
         }
-        return sp ? stack.pop(sp) : kDoneRef;
+        return sp > base ? stack.pop(sp) : kDoneRef;
     }
     if (!kAnyHit || kSortAnyHit) {
         const int nh = (tc[0] != INFINITY) + (tc[1] != INFINITY) + (tc[2] != INFINITY) + (tc[3] != INFINITY);
@@ -760,7 +765,32 @@ __device__ __forceinline__ int32_t node4_next(const Ray4 &R, uint4 a, uint4 b, u
         }
         if (have) return nxt;
     }
-    return sp ? stack.pop(sp) : kDoneRef;
+    return sp > base ? stack.pop(sp) : kDoneRef;
+}
+
+// The per-ray traversal constants of the four-wide walk (pad = the kernel's off-plane pad).
+// RT_FAST_SETUP: v_rcp_f32 (1 ulp) for the slab reciprocals; every plane of every node uses the
+// same inv, and a 1-ulp change of one axis' scale moves its slab parameters by 2^-23 relative,
+// inside the 1e-5 slack of the te <= tx test and the tcull bound.
+__device__ __forceinline__ void ray4_setup(const DevScene &sc, V3 o, V3 dir, Ray4 &R, float &pad, float &dlen) {
+    V3 inv = RT_FAST_SETUP ? mk(__builtin_amdgcn_rcpf(dir.x), __builtin_amdgcn_rcpf(dir.y), __builtin_amdgcn_rcpf(dir.z))
+                           : mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+    constexpr float kInvMax = 0x1p100f;
+    if (!(fabsf(inv.x) <= kInvMax)) inv.x = copysignf(kInvMax, dir.x);
+    if (!(fabsf(inv.y) <= kInvMax)) inv.y = copysignf(kInvMax, dir.y);
+    if (!(fabsf(inv.z) <= kInvMax)) inv.z = copysignf(kInvMax, dir.z);
+    pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
+    const float dlen2 = dot(dir, dir);
+    dlen = RT_FAST_SETUP ? 0.0f : sqrtf(dlen2);
+    // 1.00001 / |dir| with v_rsq_f32 (1 ulp) rounded up by 1e-4: never below the division form
+    R.inv_dlen = RT_FAST_SETUP ? __builtin_amdgcn_rsqf(dlen2) * 1.00011f : 0.0f;
+    R.o = o;
+    R.inv = inv;
+    R.nx = inv.x < 0; R.ny = inv.y < 0; R.nz = inv.z < 0;
+    R.pnx = R.nx ? pad : -pad; R.pny = R.ny ? pad : -pad; R.pnz = R.nz ? pad : -pad;
+    R.bnx = (R.pnx - o.x) * inv.x; R.bny = (R.pny - o.y) * inv.y; R.bnz = (R.pnz - o.z) * inv.z;
+    R.bfx = (-R.pnx - o.x) * inv.x; R.bfy = (-R.pny - o.y) * inv.y; R.bfz = (-R.pnz - o.z) * inv.z;
+    R.tcull = INFINITY;
 }
 
 template <bool kAnyHit>
@@ -771,27 +801,8 @@ __device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, 
     test_always<kAnyHit>(sc, o, dir, best, bidx, bI, done);
     if (!active || (kAnyHit && done)) return;
     Ray4 R;   // bvh4_query's per-ray constants
-    // RT_FAST_SETUP: v_rcp_f32 (1 ulp) for the slab reciprocals; every plane of every node uses the
-    // same inv, and a 1-ulp change of one axis' scale moves its slab parameters by 2^-23 relative,
-    // inside the 1e-5 slack of the te <= tx test and the tcull bound.
-    V3 inv = RT_FAST_SETUP ? mk(__builtin_amdgcn_rcpf(dir.x), __builtin_amdgcn_rcpf(dir.y), __builtin_amdgcn_rcpf(dir.z))
-                           : mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
-    constexpr float kInvMax = 0x1p100f;
-    if (!(fabsf(inv.x) <= kInvMax)) inv.x = copysignf(kInvMax, dir.x);
-    if (!(fabsf(inv.y) <= kInvMax)) inv.y = copysignf(kInvMax, dir.y);
-    if (!(fabsf(inv.z) <= kInvMax)) inv.z = copysignf(kInvMax, dir.z);
-    const float pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
-    const float dlen2 = dot(dir, dir);
-    const float dlen = RT_FAST_SETUP ? 0.0f : sqrtf(dlen2);
-    // 1.00001 / |dir| with v_rsq_f32 (1 ulp) rounded up by 1e-4: never below the division form
-    R.inv_dlen = RT_FAST_SETUP ? __builtin_amdgcn_rsqf(dlen2) * 1.00011f : 0.0f;
-    R.o = o;
-    R.inv = inv;
-    R.nx = inv.x < 0; R.ny = inv.y < 0; R.nz = inv.z < 0;
-    R.pnx = R.nx ? pad : -pad; R.pny = R.ny ? pad : -pad; R.pnz = R.nz ? pad : -pad;
-    R.bnx = (R.pnx - o.x) * inv.x; R.bny = (R.pny - o.y) * inv.y; R.bnz = (R.pnz - o.z) * inv.z;
-    R.bfx = (-R.pnx - o.x) * inv.x; R.bfy = (-R.pny - o.y) * inv.y; R.bfz = (-R.pnz - o.z) * inv.z;
-    R.tcull = INFINITY;
+    float pad, dlen;
+    ray4_setup(sc, o, dir, R, pad, dlen);
     int sp = 0;
     int32_t node = 0;          // inner node to visit, a leaf ref, or kDoneRef
     int32_t leaf = kDoneRef;   // the postponed leaf
@@ -846,6 +857,160 @@ __device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, 
             }
         }
         if (node == kDoneRef) break;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// While-while walk with in-wave work stealing (RT_TUNE_WAVE_STEAL, chain launch): a lane whose own query is finished
+// takes the bottom entry of another lane's traversal stack (a subtree that lane would visit later)
+// together with that lane's ray, walks it with the same node and triangle arithmetic, and folds
+// what it finds into the ray owner's (distance, index) key in LDS. Exactness: every subtree is
+// walked by exactly one lane; a helper culls with its own best, which starts at the donor's best
+// (an upper bound of the final minimum), so no triangle that could beat the final minimum is
+// skipped; the result is the lexicographic minimum of all keys. The owner takes its own hit point
+// when its own key wins, else re-runs test_triangle on the winning record (the same arithmetic on
+// the same record and ray, so the same bits). Any-hit: any key is a hit; the owner stops walking
+// once a helper has published one. Only placement changes, never results.
+// ---------------------------------------------------------------------------------------------
+#ifndef RT_STEAL_WPE
+#define RT_STEAL_WPE 4   // waves per EU of the stealing chain kernel (5 spills ~100 VGPRs: measured slower)
+#endif
+#ifndef RT_STEAL_MIN_IDLE
+#define RT_STEAL_MIN_IDLE 8   // steal only when at least this many lanes of the wave are idle
+#endif
+#ifndef RT_STEAL_TOP
+#define RT_STEAL_TOP 1        // 1: a donor gives its nearest pending subtree (top of stack); 0: its farthest
+#endif
+constexpr unsigned long long kNoKey = ~0ull;
+__device__ __forceinline__ unsigned long long hit_key(float best, int bidx) {
+    return (static_cast<unsigned long long>(__float_as_uint(best)) << 32) | static_cast<uint32_t>(bidx);
+}
+
+template <bool kAnyHit>
+__device__ __forceinline__ void bvh4_query_steal(const DevScene &sc, V3 o, V3 dir, bool active, int &bidx, V3 &bI,
+                                                 const LaneStack &stack, unsigned &tests, unsigned &visits) {
+    __shared__ unsigned long long s_key[kBvhBlock];   // per lane: its ray's best key (own walk and helpers)
+    __shared__ float s_hit[3 * kBvhBlock];            // per lane: the hit point of that key
+    __shared__ int32_t s_xfer[2 * kBvhBlock];         // per wave: [pair rank] donor lane | owner << 8, stolen ref
+    const int tid = static_cast<int>(threadIdx.x), lane = __lane_id(), wb = tid & ~63;   // this wave's slots
+    float best = FLT_MAX;
+    bool done = !active;
+    test_always<kAnyHit>(sc, o, dir, best, bidx, bI, done);
+    s_key[tid] = kNoKey;
+    // o, dir: the ray this lane walks (its own, later the rays it helps with)
+    Ray4 R;
+    float pad, dlen;
+    ray4_setup(sc, o, dir, R, pad, dlen);
+    int sp = 0, base = 0;
+    int32_t node = (active && !(kAnyHit && done)) ? 0 : kDoneRef;
+    int32_t leaf = kDoneRef;
+    int owner = active ? tid : -1;   // the slot this walk reports to (its own, or the helped lane's); -1: idle
+    int pidx = -1;                   // bidx as last published or adopted: a different bidx is a new find
+    __builtin_amdgcn_wave_barrier();
+    while (true) {
+        // new finds go to the ray's slot: the key first, then (second pass) the hit point of the
+        // winning key (equal keys: the same triangle and ray, so the same point)
+        const bool pub = owner >= 0 && bidx != pidx;
+        const unsigned long long k = hit_key(best, bidx);
+        if (pub) atomicMin(&s_key[owner], k);
+        __builtin_amdgcn_wave_barrier();
+        if (pub && s_key[owner] == k) {
+            s_hit[3 * owner] = bI.x; s_hit[3 * owner + 1] = bI.y; s_hit[3 * owner + 2] = bI.z;
+        }
+        if (pub) pidx = bidx;
+        if (owner >= 0) {   // a better key from another walk of the same ray: cull with it
+            const unsigned long long sk = s_key[owner];
+            if (sk < hit_key(best, bidx)) {
+                if (kAnyHit) { node = kDoneRef; leaf = kDoneRef; }   // any hit ends every walk of the ray
+                best = __uint_as_float(static_cast<uint32_t>(sk >> 32));
+                bidx = static_cast<int>(static_cast<uint32_t>(sk));
+                pidx = bidx;
+                if (!kAnyHit) R.tcull = cull_param(R, best, pad, dlen);
+            }
+        }
+        if (node == kDoneRef && leaf == kDoneRef) { owner = -1; sp = base; }   // (an abandoned any-hit walk's stack too)
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t act = __ballot(1), idle = __ballot(owner < 0);
+        if (idle == act) break;
+        const uint64_t donors = __ballot(owner >= 0 && sp - base >= 1);
+        if (__popcll(idle) >= RT_STEAL_MIN_IDLE && donors) {
+            const int np = min(__popcll(idle), __popcll(donors));
+            const uint64_t lt = (1ull << lane) - 1ull;
+            const int ir = __popcll(idle & lt), dr = __popcll(donors & lt);
+            if (((donors >> lane) & 1ull) && dr < np) {
+                s_xfer[wb + 2 * dr] = lane | (owner << 8);
+                if (RT_STEAL_TOP) {   // the top entry: the nearest subtree still pending
+                    --sp;
+                    s_xfer[wb + 2 * dr + 1] = stack.at(sp);
+                } else {              // the bottom entry: the farthest
+                    s_xfer[wb + 2 * dr + 1] = stack.at(base);
+                    ++base;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            const bool helper = ((idle >> lane) & 1ull) && ir < np;
+            int src = lane, xo = -1, ref = kDoneRef;
+            if (helper) {
+                const int v = s_xfer[wb + 2 * ir];
+                src = v & 0xFF;
+                xo = v >> 8;
+                ref = s_xfer[wb + 2 * ir + 1];
+            }
+            __builtin_amdgcn_wave_barrier();
+            const V3 ho = mk(__shfl(o.x, src), __shfl(o.y, src), __shfl(o.z, src));
+            const V3 hd = mk(__shfl(dir.x, src), __shfl(dir.y, src), __shfl(dir.z, src));
+            const float hb = __shfl(best, src);
+            const int hi = __shfl(bidx, src);
+            if (helper) {
+                o = ho; dir = hd;
+                best = hb; bidx = hi; pidx = hi;   // the donor's best bounds the final minimum: cull with it
+                ray4_setup(sc, o, dir, R, pad, dlen);
+                if (!kAnyHit && best < FLT_MAX) R.tcull = cull_param(R, best, pad, dlen);
+                done = false;
+                sp = 0; base = 0;
+                node = ref;
+                if (node < 0) { leaf = node; node = kDoneRef; }   // a leaf ref
+                owner = xo;
+            }
+        }
+        while (node >= 0) {
+            ++visits;
+            uint4 a, b, c, d;
+            load_node4(stack, sc.nodes4, node, a, b, c, d);
+            node = node4_next<kAnyHit>(R, a, b, c, d, stack, sp, base);
+            if (node < 0 && node != kDoneRef && leaf == kDoneRef) {   // postpone it, keep walking
+                leaf = node;
+                node = sp > base ? stack.pop(sp) : kDoneRef;
+            }
+            if (__all(leaf != kDoneRef)) break;
+        }
+        while (leaf != kDoneRef) {
+            const uint32_t u = static_cast<uint32_t>(leaf);
+            const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
+            const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
+            const TriRec T = leaf_rec(sc, first);
+            test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first]), o, dir, best, bidx, bI, done);
+            ++tests;
+            if (kAnyHit && done) { node = kDoneRef; leaf = kDoneRef; break; }
+            if (cnt > 1) {
+                leaf = static_cast<int32_t>(u + 1u - (1u << kBvhCountShift));
+                continue;
+            }
+            if (!kAnyHit && best < FLT_MAX) R.tcull = cull_param(R, best, pad, dlen);
+            leaf = kDoneRef;
+            if (node < 0 && node != kDoneRef) {
+                leaf = node;
+                node = sp > base ? stack.pop(sp) : kDoneRef;
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const unsigned long long k = s_key[tid];
+    bidx = -1;
+    bI = mk(0, 0, 0);   // no hit: the callers' initial point (every call site starts from (0, 0, 0))
+    if (active && k != kNoKey) {
+        bidx = static_cast<int>(static_cast<uint32_t>(k));
+        bI = mk(s_hit[3 * tid], s_hit[3 * tid + 1], s_hit[3 * tid + 2]);
     }
 }
 
@@ -1088,7 +1253,7 @@ struct TreeArgs {
     const uint32_t *idx;
 };
 
-template <bool kAnyHit, int W>
+template <bool kAnyHit, int W, bool kSteal = false>
 __device__ __forceinline__ void bvh_query_w(const DevScene &sc, const Bvh4Node *__restrict__ n4,
                                             const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx,
                                             int32_t *lds, V3 o, V3 dir, bool active, int &bidx, V3 &bI,
@@ -1096,6 +1261,7 @@ __device__ __forceinline__ void bvh_query_w(const DevScene &sc, const Bvh4Node *
                                             Stamps *st = nullptr) {
     if (W == 5) wave_query<kAnyHit>(sc, n4, lrec, lidx, o, dir, active, bidx, bI, lds + (threadIdx.x >> 6) * sc.bvh4_stack,
                                     tests, visits);
+    else if (W == 4 && kSteal && !st) bvh4_query_steal<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
     else if (W == 4 && RT_WHILE_WHILE && !st) bvh4_query_ww<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
     else if (W == 4) bvh4_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits, st);
     else bvh_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
@@ -1843,7 +2009,7 @@ constexpr int kChainSteps = 256;   // max_lvl <= 254
 // One chain step of one sample (trace, raytracing.cpp:381-406): the closest-hit query, isShadow
 // per light (:241-261), shade (:335-368). Returns the secondary ray (state kChildTrace) or the end
 // of the chain. Shadow-ray statistics are counted per block in s_sh.
-template <bool kAnyHit, int W, bool kCount, bool kInLane = false>
+template <bool kAnyHit, int W, bool kCount, bool kInLane = false, bool kSteal = false>
 __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeParams &p, const DevWork &w, int step,
                                                 int sample, V3 org, V3 dst, int lvl, const LaneStack &stack,
                                                 int32_t *lds_stack, const Bvh4Node *__restrict__ n4,
@@ -1854,7 +2020,7 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
     none.local = mk(0, 0, 0);   // trace() miss: black (:389-391)
     int bidx = -1;
     V3 bI = mk(0, 0, 0);
-    bvh_query_w<false, W>(sc, n4, lrec, lidx, lds_stack, org, sub(dst, org), true, bidx, bI, stack, wc.tests, wc.visits);
+    bvh_query_w<false, W, kSteal>(sc, n4, lrec, lidx, lds_stack, org, sub(dst, org), true, bidx, bI, stack, wc.tests, wc.visits);
     if (bidx >= sc.nt) { w.counters[kErrorSlot] = 1; bidx = -1; }
     if (bidx < 0) {
         if (!kInLane) shade_miss(w, step, sample);
@@ -1883,7 +2049,7 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
             int sidx = -1;
             V3 sI = mk(0, 0, 0);
             const V3 sd = mk(p.lights[l][0] - so.x, p.lights[l][1] - so.y, p.lights[l][2] - so.z);
-            bvh_query_w<kAnyHit, W>(sc, n4, lrec, lidx, lds_stack, so, sd, true, sidx, sI, stack, ws.tests, ws.visits);
+            bvh_query_w<kAnyHit, W, kSteal>(sc, n4, lrec, lidx, lds_stack, so, sd, true, sidx, sI, stack, ws.tests, ws.visits);
             if (sidx >= 0 && !sc.mats[sc.tri_mat[sidx]].transparent) mask |= 1u << l;   // :253-257
         }
     }
@@ -1900,8 +2066,8 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
 // w.batch_order[v]; every wave records its batch's duration in w.batch_cost, from which
 // launch_order_batches prepares the next launch's order (longest first, so the deep reflection
 // chains of a frame start at once instead of trailing it). Placement never changes results.
-template <int W, bool kAnyHit, bool kCount, bool kInLane = false>
-__global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CHAIN_WPE))) void k_chain(
+template <int W, bool kAnyHit, bool kCount, bool kInLane = false, bool kSteal = false>
+__global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kSteal ? RT_STEAL_WPE : RT_CHAIN_WPE))) void k_chain(
     const DevScene sc, const ShadeParams p, DevWork w, int first, const Bvh4Node *__restrict__ n4,
     const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx, int ordered, uint8_t *__restrict__ out_u8,
     float *__restrict__ out_f32, int fuse_spp, const FrameGeom g) {
@@ -1953,7 +2119,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
 #endif
         for (int step = first; step < kChainSteps; ++step) {
             if (step > first) atomicAdd(&s_q[step], 1);
-            const Secondary sec = chain_step<kAnyHit, W, kCount, kInLane>(sc, p, w, step, sample, org, dst, lvl, stack,
+            const Secondary sec = chain_step<kAnyHit, W, kCount, kInLane, kSteal>(sc, p, w, step, sample, org, dst, lvl, stack,
                                                                           lds_stack, n4, lrec, lidx, s_sh, wc, ws);
             if (sec.state != kChildTrace) {
                 if (kInLane)   // the chain ends here: fold it in the lane (fold_chain's arithmetic)
@@ -2459,8 +2625,15 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
     if (inlane)
         k = wide ? (s.any_transparent ? k_chain<4, false, false, true> : k_chain<4, true, false, true>)
                  : (s.any_transparent ? k_chain<2, false, false, true> : k_chain<2, true, false, true>);
+    // in-wave work stealing (RT_TUNE_WAVE_STEAL; 2 = when the launch is at most two rounds of
+    // resident waves, where a few long walks set the frame time): four-wide, in-lane chains
+    const int64_t resident_lanes = static_cast<int64_t>(std::max(s.refill_grid, 1)) * kBvhBlock;
+    const bool steal = wide && inlane && (s.wave_steal == 1 || (s.wave_steal == 2 && capacity <= 2 * resident_lanes));
+    if (steal) k = s.any_transparent ? k_chain<4, false, false, true, true> : k_chain<4, true, false, true, true>;
 #ifndef RT_WAVE_TIMES   // (the wave-times diagnostic build times the uncounted kernel)
-    if (s.work && inlane)
+    if (s.work && inlane && steal)
+        k = s.any_transparent ? k_chain<4, false, true, true, true> : k_chain<4, true, true, true, true>;
+    else if (s.work && inlane)
         k = wide ? (s.any_transparent ? k_chain<4, false, true, true> : k_chain<4, true, true, true>)
                  : (s.any_transparent ? k_chain<2, false, true, true> : k_chain<2, true, true, true>);
     else if (s.work)

@@ -383,7 +383,9 @@ def test_multi_frame_shard_batch_reassembles(workdir, gpu_available):
                                    {"chain_split": 1}, {"chain_split": 2}, {"chain_refill": 1},
                                    {"chain_refill": 1, "batch_order": 0}, {"chain_refill": 1, "refill_grid": 1},
                                    {"chain_refill": 1, "refill_grid": 3}, {"chain_refill": 1, "refill_grid": 7, "lds_stack": 1},
-                                   {"chain_refill": 1, "refill_grid": 5, "bvh_width": 2}])
+                                   {"chain_refill": 1, "refill_grid": 5, "bvh_width": 2}, {"wave_steal": 0},
+                                   {"wave_steal": 1}, {"wave_steal": 1, "lds_stack": 1},
+                                   {"wave_steal": 1, "bvh_grid": 3}, {"wave_steal": 1, "top_nodes": 0}])
 def test_launch_shape_knobs_never_change_results(knobs, workdir, gpu_available):
     """Query distribution (grid-stride, static XCD segments, work-stealing XCD queues), tiny grids
     (fewer blocks than XCDs), tree width and the LDS/HBM split of the traversal stack (1 entry in
@@ -398,6 +400,26 @@ def test_launch_shape_knobs_never_change_results(knobs, workdir, gpu_available):
         u8, f32, c = sc.render(p, want_f32=True)
     assert [int(x) for x in c] == [int(x) for x in refc]
     assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
+
+
+@pytest.mark.parametrize("spec,w,h,pf,lights", [("ref:dodgeColorTest.obj", 800, 600, 1, 1), ("syn:F4", 160, 90, 2, 2),
+                                                ("syn:C4", 480, 270, 1, 2), ("ref:Models/shadow_test.obj", 200, 150, 2, 4)])
+def test_wave_steal_matches_plain_walk(spec, w, h, pf, lights, workdir, gpu_available):
+    """RT_TUNE_WAVE_STEAL: lanes whose query is done walk subtrees of other lanes' stacks with those
+    lanes' rays and fold their finds into the owner's (distance, index) key. The C2 frame (the car's
+    slivers and always-list), transparency (closest-hit shadows), pf 2 and up to four lights:
+    frames, floats and ray counts equal the plain walk's, and the plain walk equals the oracle on
+    sampled pixels elsewhere in the suite."""
+    L = [[0, 0, 4], [1.5, 1.5, 4], [-1.5, 1.5, 4], [0, -1.5, 4]][:lights]
+    p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=3 if lights > 1 else 1, lights=L)
+    with R.Scene.load(scene_path(spec, workdir), device=0) as sc:
+        sc.tune("wave_steal", 0)
+        ref, reff, refc = sc.render(p, want_f32=True)
+        sc.tune("wave_steal", 1)
+        for _ in range(2):
+            u8, f32, c = sc.render(p, want_f32=True)
+            assert [int(x) for x in c] == [int(x) for x in refc]
+            assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
 
 
 @pytest.mark.parametrize("spec,w,h,pf,flags", [("syn:C4", 333, 187, 1, 0), ("syn:C4", 160, 90, 2, 0),
