@@ -279,9 +279,11 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
                                     10 per CU) */
 #define RT_TUNE_WAVE_STEAL 21    /* in-wave work stealing in the chain launch: a lane whose query is done
                                     walks a subtree from another lane's stack with that lane's ray
-                                    (four-wide tree). 0 off, 1 on, 2 (default) when the launch is at most
-                                    two rounds of resident waves (a few long walks set the frame time:
-                                    C2 0.24 -> 0.18 ms; C4, six rounds, is faster without) */
+                                    (four-wide tree). 0 off, 1 on, 2 (default, auto): the third and
+                                    fourth launches over a frame geometry are timed without and with it
+                                    and later ones use the faster (before that: on when the launch is at
+                                    most two rounds of resident waves). C2 0.24 -> 0.18 ms, C3 -4%;
+                                    C4 is faster without */
 #define RT_TUNE_TOP_NODES 13     /* four-wide nodes of the tree's top levels (breadth-first, the first
                                     ones in the node array) each block reads from an LDS copy (0-85) */
 #define RT_TUNE_CHAIN_SPLIT 12   /* query distribution of the chain launch: as RT_TUNE_XCD_SPLIT, or 3: 64-query

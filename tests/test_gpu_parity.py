@@ -422,6 +422,20 @@ def test_wave_steal_matches_plain_walk(spec, w, h, pf, lights, workdir, gpu_avai
             assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
 
 
+def test_wave_steal_auto_trials_keep_results(workdir, gpu_available):
+    """RT_TUNE_WAVE_STEAL 2 (default): launches 3 and 4 over a frame geometry are timed without and
+    with stealing, later ones use the faster; every render of the sequence equals the plain walk's."""
+    p = R.RenderParams(width=400, height=300, pf=1, max_lvl=1, lights=[[0, 0, 4]])
+    with R.Scene.load(scene_path("ref:dodgeColorTest.obj", workdir), device=0) as sc:
+        sc.tune("wave_steal", 0)
+        ref, reff, refc = sc.render(p, want_f32=True)
+        sc.tune("wave_steal", 2)
+        for _ in range(8):
+            u8, f32, c = sc.render(p, want_f32=True)
+            assert [int(x) for x in c] == [int(x) for x in refc]
+            assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
+
+
 @pytest.mark.parametrize("spec,w,h,pf,flags", [("syn:C4", 333, 187, 1, 0), ("syn:C4", 160, 90, 2, 0),
                                                ("syn:F4", 96, 54, 3, 0), ("ref:dodgeColorTest.obj", 200, 150, 1, 0),
                                                ("syn:F3", 70, 41, 2, 1 << 8), ("syn:F4", 17, 9, 1, 0)])
