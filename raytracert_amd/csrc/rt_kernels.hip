@@ -629,6 +629,10 @@ __device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, boo
 #endif
 constexpr int32_t kDoneRef = kBvhEmpty;   // "no ref": a count-0 leaf is never a wanted child
 
+#ifndef RT_NF_PACKED
+#define RT_NF_PACKED 0   // 1: near/far slab planes as v_pk_fma_f32 pairs (node block 140 -> 125 VALU, yet C4
+                         // 0.481 -> 0.494 ms and C5 8.89 -> 9.30 ms: profiles/r02_ab_nf_packed.txt)
+#endif
 #ifndef RT_NODE_V2
 #define RT_NODE_V2 1   // per-ray slab offsets folded into one FMA per plane; exponent by v_ldexp_f32
 #endif
@@ -690,9 +694,24 @@ __device__ __forceinline__ int32_t node4_next(const Ray4 &R, uint4 a, uint4 b, u
     float tc[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const float tnx = q_decode(cnx, kx, wnx, k), tfx = q_decode(cfx, kx, wfx, k);
-        const float tny = q_decode(cny, ky, wny, k), tfy = q_decode(cfy, ky, wfy, k);
-        const float tnz = q_decode(cnz, kz, wnz, k), tfz = q_decode(cfz, kz, wfz, k);
+        float tnx, tfx, tny, tfy, tnz, tfz;
+        if (RT_NF_PACKED) {   // near and far plane of one axis in one v_pk_fma_f32 (same per-lane FMAs)
+            typedef float f2v __attribute__((ext_vector_type(2)));
+            const f2v px = __builtin_elementwise_fma(
+                f2v{static_cast<float>((wnx >> (8 * k)) & 0xFFu), static_cast<float>((wfx >> (8 * k)) & 0xFFu)},
+                f2v{kx, kx}, f2v{cnx, cfx});
+            const f2v py = __builtin_elementwise_fma(
+                f2v{static_cast<float>((wny >> (8 * k)) & 0xFFu), static_cast<float>((wfy >> (8 * k)) & 0xFFu)},
+                f2v{ky, ky}, f2v{cny, cfy});
+            const f2v pz = __builtin_elementwise_fma(
+                f2v{static_cast<float>((wnz >> (8 * k)) & 0xFFu), static_cast<float>((wfz >> (8 * k)) & 0xFFu)},
+                f2v{kz, kz}, f2v{cnz, cfz});
+            tnx = px.x; tfx = px.y; tny = py.x; tfy = py.y; tnz = pz.x; tfz = pz.y;
+        } else {
+            tnx = q_decode(cnx, kx, wnx, k); tfx = q_decode(cfx, kx, wfx, k);
+            tny = q_decode(cny, ky, wny, k); tfy = q_decode(cfy, ky, wfy, k);
+            tnz = q_decode(cnz, kz, wnz, k); tfz = q_decode(cfz, kz, wfz, k);
+        }
         const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
         const float tx = fminf(fminf(tfx, tfy), tfz);
         bool h = te <= tx * 1.00001f;
