@@ -279,8 +279,8 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
                                     10 per CU) */
 #define RT_TUNE_WAVE_STEAL 21    /* in-wave work stealing in the chain launch: a lane whose query is done
                                     walks a subtree from another lane's stack with that lane's ray
-                                    (four-wide tree). 0 off, 1 on, 2 (default, auto): the third and
-                                    fourth launches over a frame geometry are timed without and with it
+                                    (four-wide tree). 0 off, 1 on, 2 (default, auto): the second and
+                                    third launches over a frame geometry are timed without and with it
                                     and later ones use the faster (before that: on when the launch is at
                                     most two rounds of resident waves). C2 0.24 -> 0.18 ms, C3 -4%;
                                     C4 is faster without */

@@ -423,7 +423,7 @@ def test_wave_steal_matches_plain_walk(spec, w, h, pf, lights, workdir, gpu_avai
 
 
 def test_wave_steal_auto_trials_keep_results(workdir, gpu_available):
-    """RT_TUNE_WAVE_STEAL 2 (default): launches 3 and 4 over a frame geometry are timed without and
+    """RT_TUNE_WAVE_STEAL 2 (default): launches 2 and 3 over a frame geometry are timed without and
     with stealing, later ones use the faster; every render of the sequence equals the plain walk's."""
     p = R.RenderParams(width=400, height=300, pf=1, max_lvl=1, lights=[[0, 0, 4]])
     with R.Scene.load(scene_path("ref:dodgeColorTest.obj", workdir), device=0) as sc:
