@@ -436,6 +436,19 @@ __device__ __forceinline__ void cswap(float &ta, int32_t &ra, float &tb, int32_t
 // [5] whole queries. The stamps serialise the loop (s_waitcnt before each), so they split a step's
 // time into its parts; they do not measure the production schedule.
 struct Stamps { unsigned long long v[6]; };
+
+// Diagnostic build only (-DRT_REGION_COUNTS): wave-level iteration counts of the chain kernel's
+// regions and the active lanes they ran with, summed per block in LDS and added to the diagnostic
+// words (rt_diag_read [0, 32)): [r] wave iterations, [16 + r] active lanes. r: 0 chain step,
+// 1 closest-hit query, 2 shadow query, 3 closest-hit node iteration, 4 closest-hit leaf iteration,
+// 5 shadow node iteration, 6 shadow leaf iteration, 7 shade. tools/region_counts.py reads them.
+#ifdef RT_REGION_COUNTS
+__shared__ unsigned long long g_rc[32];
+#define RT_RC(r) do { const uint64_t m_ = __ballot(1); \
+    if (__lane_id() == __builtin_ctzll(m_)) { atomicAdd(&g_rc[(r)], 1ull); atomicAdd(&g_rc[16 + (r)], static_cast<unsigned long long>(__popcll(m_))); } } while (0)
+#else
+#define RT_RC(r) do { } while (0)
+#endif
 #ifdef RT_STAMPS
 constexpr bool kStamps = true;
 #else
@@ -819,6 +832,7 @@ __device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, 
     bool done = !active;
     test_always<kAnyHit>(sc, o, dir, best, bidx, bI, done);
     if (!active || (kAnyHit && done)) return;
+    RT_RC(kAnyHit ? 2 : 1);
     Ray4 R;   // bvh4_query's per-ray constants
     float pad, dlen;
     ray4_setup(sc, o, dir, R, pad, dlen);
@@ -828,6 +842,7 @@ __device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, 
     int32_t leaf2 = kDoneRef;  // a second one (RT_WW_LEAVES 2)
     while (true) {
         while (node >= 0) {
+            RT_RC(kAnyHit ? 5 : 3);
             ++visits;
             uint4 a, b, c, d;
             load_node4(stack, sc.nodes4, node, a, b, c, d);
@@ -846,6 +861,7 @@ __device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, 
                 break;
         }
         while (leaf != kDoneRef) {
+            RT_RC(kAnyHit ? 6 : 4);
             const uint32_t u = static_cast<uint32_t>(leaf);
             const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
             const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
@@ -2034,6 +2050,7 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
                                                 int32_t *lds_stack, const Bvh4Node *__restrict__ n4,
                                                 const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx,
                                                 int *s_sh, WorkTally<kCount> &wc, WorkTally<kCount> &ws) {
+    RT_RC(0);
     Secondary none;
     none.state = kChildNone;
     none.local = mk(0, 0, 0);   // trace() miss: black (:389-391)
@@ -2072,6 +2089,7 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
             if (sidx >= 0 && !sc.mats[sc.tri_mat[sidx]].transparent) mask |= 1u << l;   // :253-257
         }
     }
+    RT_RC(7);
     return shade_hit<kInLane>(sc, p, w, step, sample, sub(dst, org), lvl, bidx, bI, [&](int l) { return ((mask >> l) & 1u) != 0; });
 }
 
@@ -2094,6 +2112,9 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
     extern __shared__ int32_t lds_stack[];
     __shared__ int s_q[kChainSteps], s_sh[kChainSteps];
     for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) { s_q[i] = 0; s_sh[i] = 0; }
+#ifdef RT_REGION_COUNTS
+    if (threadIdx.x < 32) g_rc[threadIdx.x] = 0;
+#endif
     __syncthreads();
     const LaneStack stack = lane_stack(sc, lds_stack);
     WorkTally<kCount> wc, ws;   // closest-hit and shadow work (totals only: lanes diverge here)
@@ -2184,6 +2205,9 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         if (s_q[i]) atomicAdd(&w.counters[i], s_q[i]);
         if (s_sh[i]) atomicAdd(&w.counters[kMaxStepsCounters + i], s_sh[i]);
     }
+#ifdef RT_REGION_COUNTS
+    if (threadIdx.x < 32 && sc.work && g_rc[threadIdx.x]) atomicAdd(&sc.work[2 * kWorkFields + threadIdx.x], g_rc[threadIdx.x]);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2305,6 +2329,9 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CH
         if (s_q[i]) atomicAdd(&w.counters[i], s_q[i]);
         if (s_sh[i]) atomicAdd(&w.counters[kMaxStepsCounters + i], s_sh[i]);
     }
+#ifdef RT_REGION_COUNTS
+    if (threadIdx.x < 32 && sc.work && g_rc[threadIdx.x]) atomicAdd(&sc.work[2 * kWorkFields + threadIdx.x], g_rc[threadIdx.x]);
+#endif
 }
 
 // Frame: per pixel, sum sub-samples (subx outer, suby inner), divide by pf^2 (main.cpp:391),
@@ -2649,7 +2676,7 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
     const int64_t resident_lanes = static_cast<int64_t>(std::max(s.refill_grid, 1)) * kBvhBlock;
     const bool steal = wide && inlane && (s.wave_steal == 1 || (s.wave_steal == 2 && capacity <= 2 * resident_lanes));
     if (steal) k = s.any_transparent ? k_chain<4, false, false, true, true> : k_chain<4, true, false, true, true>;
-#ifndef RT_WAVE_TIMES   // (the wave-times diagnostic build times the uncounted kernel)
+#if !defined(RT_WAVE_TIMES) && !defined(RT_REGION_COUNTS)   // (diagnostic builds run the uncounted kernel)
     if (s.work && inlane && steal)
         k = s.any_transparent ? k_chain<4, false, true, true, true> : k_chain<4, true, true, true, true>;
     else if (s.work && inlane)
