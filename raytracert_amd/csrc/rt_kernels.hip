@@ -913,6 +913,12 @@ __device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, 
 #ifndef RT_STEAL_MIN_IDLE
 #define RT_STEAL_MIN_IDLE 8   // steal only when at least this many lanes of the wave are idle
 #endif
+#ifndef RT_STEAL_SPLIT
+#define RT_STEAL_SPLIT 512   // at most this many of the longest batches run as two half waves (k_chain)
+#endif
+#ifndef RT_STEAL_SPLIT_DIV
+#define RT_STEAL_SPLIT_DIV 32   // ... and at most this fraction (1 / DIV) of them
+#endif
 #ifndef RT_STEAL_TOP
 #define RT_STEAL_TOP 1        // 1: a donor gives its nearest pending subtree (top of stack); 0: its farthest
 #endif
@@ -2107,7 +2113,7 @@ template <int W, bool kAnyHit, bool kCount, bool kInLane = false, bool kSteal = 
 __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kSteal ? RT_STEAL_WPE : RT_CHAIN_WPE))) void k_chain(
     const DevScene sc, const ShadeParams p, DevWork w, int first, const Bvh4Node *__restrict__ n4,
     const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx, int ordered, uint8_t *__restrict__ out_u8,
-    float *__restrict__ out_f32, int fuse_spp, const FrameGeom g) {
+    float *__restrict__ out_f32, int fuse_spp, const FrameGeom g, int split) {
     constexpr bool kInlinePrimary = kInLane && RT_PRIMARY_INLINE;
     extern __shared__ int32_t lds_stack[];
     __shared__ int s_q[kChainSteps], s_sh[kChainSteps];
@@ -2126,9 +2132,18 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
 #endif
     const int nq = kInlinePrimary ? static_cast<int>(static_cast<int64_t>(g.ntiles) * g.tw * g.th * g.pfx * g.pfy)
                                   : w.counters[first];
-    drive_queries(nq, sc.chain_split & 3, w.wq + (2 * first) * kWqSlot, [&](int j0, int end) {
+    // split (ordered launches of the stealing kernel): the first `split` batches of the order (the
+    // longest) run as two waves of 32 samples each, so the other 32 lanes of each are free to
+    // steal subtrees of the long walks from the start; virtual wave vb < 2 * split is half vb & 1
+    // of batch order[vb >> 1], later ones batch order[vb - split]
+    drive_queries(nq + split * kWave, sc.chain_split & 3, w.wq + (2 * first) * kWqSlot, [&](int j0, int vend) {
+        const int end = vend - split * kWave;
         const int vb = j0 >> 6;   // this wave's batch in dispatch order (wave-uniform when ordered)
-        const int pb = (ordered && (vb << 6) < end) ? w.batch_order[vb] : vb;
+        const bool half = ordered && vb < 2 * split;
+        const int ob = half ? (vb >> 1) : vb - (ordered ? split : 0);
+        const int pb = (ordered && (vb << 6) < vend) ? w.batch_order[ob] : vb;
+        const int lane_off = half ? ((vb & 1) * (kWave / 2) + __lane_id()) : (j0 & (kWave - 1));
+        const bool lane_on = !half || __lane_id() < kWave / 2;
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         V3 rgb = mk(0, 0, 0);   // fused pixels: this lane's folded chain and its pixel (valid samples)
         int px = -1;
@@ -2175,7 +2190,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
             if (!kInLane) rgb = fold_chain(w, sample);
             px = kInlinePrimary ? static_cast<int>(pxi) : w.pix_out[sample];
         }
-        }(ordered ? pb * kWave + (j0 & (kWave - 1)) : j0);
+        }(!lane_on ? end : ordered ? pb * kWave + lane_off : j0);
         if (fuse_spp) {   // k_frame's arithmetic: a pixel's fuse_spp sub-samples sit in adjacent lanes
             const int lane = __lane_id(), base = lane & ~(fuse_spp - 1);
             V3 acc = mk(0, 0, 0);
@@ -2185,7 +2200,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
             acc = mk(acc.x / div, acc.y / div, acc.z / div);   // operator/, Vec3D.h:36-38
             if (lane == base && px >= 0) store_pixel(acc, 3 * static_cast<int64_t>(px), out_u8, out_f32);
         }
-        if (__lane_id() == 0 && j0 < end)
+        if (__lane_id() == 0 && j0 < vend)
             w.batch_cost[pb] = static_cast<uint32_t>(min(__builtin_amdgcn_s_memrealtime() - t0, 0xFFFFFFFFull));
     });
 #ifdef RT_WAVE_TIMES
@@ -2699,8 +2714,12 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
                            s.leaf_idx, out_u8, out_f32, geom);
         return;
     }
-    hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, p, w, first,
-                       s.nodes4, s.leaf_recs, s.leaf_idx, ordered ? 1 : 0, out_u8, out_f32, fuse_spp, geom);
+    // the stealing kernel, ordered over grid-stride batches: the longest batches run as half waves
+    const int split = (steal && ordered && (s.chain_split & 7) == 0 && RT_STEAL_SPLIT > 0)
+                          ? static_cast<int>(std::min<int64_t>((capacity + kWave - 1) / kWave / RT_STEAL_SPLIT_DIV, RT_STEAL_SPLIT)) : 0;
+    hipLaunchKernelGGL(k, dim3(grid_bvh(capacity + static_cast<int64_t>(split) * kWave, s.bvh_grid)), dim3(kBvhBlock),
+                       bvh_lds(s), stream, s, p, w, first, s.nodes4, s.leaf_recs, s.leaf_idx, ordered ? 1 : 0, out_u8,
+                       out_f32, fuse_spp, geom, split);
 }
 
 int chain_blocks_per_cu() { return 4 * RT_CHAIN_WPE * kWave / kBvhBlock; }

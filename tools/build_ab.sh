@@ -9,11 +9,14 @@ HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast
 while [ $# -ge 2 ]; do
   N=$1; D=$2; shift 2
   /opt/rocm/bin/hipcc $HIPFLAGS $D -c csrc/rt_kernels.hip -o ab/k_$N.o &
+  # BVH builder knobs (RT_BVH_*) need their own bvh.o
+  case "$D" in *RT_BVH_*) /opt/rocm/bin/hipcc $HIPFLAGS -pthread $D -c csrc/bvh.cpp -o ab/b_$N.o & ;; esac
 done
 wait
 for o in ab/k_*.o; do
   N=${o#ab/k_}; N=${N%.o}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -pthread -o ab/lib_$N.so $o build/rt_capi.o build/rt_comm.o build/scene_loader.o build/obj_parallel.o build/bvh.o -ldl
-  rm -f $o
+  B=build/bvh.o; [ -f ab/b_$N.o ] && B=ab/b_$N.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -pthread -o ab/lib_$N.so $o build/rt_capi.o build/rt_comm.o build/scene_loader.o build/obj_parallel.o $B -ldl
+  rm -f $o ab/b_$N.o
 done
 ls ab
