@@ -202,6 +202,8 @@ def main():
                 self.frames_out = [torch.zeros(1, dtype=torch.uint8, device=dev)] * 2
             self.nfin = 0
             self.pending = []
+            # rank 0 un-permutes on a side stream, so the next step's render is not queued behind it
+            self.side = torch.cuda.Stream(dev) if (rank == 0 and not frame_path) else None
 
         def render_shard(self, want_counts=False, buf=None):
             # one call: this rank's tile ids rank, rank + N, ... over the step's `frames` frames
@@ -220,7 +222,9 @@ def main():
             return self.render_shard(buf=self.bufs[i % 2])
 
         def finish(self, p):
-            # order the stream after the gather, then un-permute on rank 0 (the library's kernel)
+            # order the render stream after the gather (the next render reuses the gathered shard
+            # buffer; the gather is long done by then), then un-permute on rank 0's side stream
+            # (the library's kernel), which waits for the same point
             gathered, work = p
             if work is not None:
                 work.wait()
@@ -228,8 +232,12 @@ def main():
                 return None
             out = self.frames_out[self.nfin % 2]
             self.nfin += 1
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            self.side.wait_event(ev)
+            gathered.record_stream(self.side)
             R.assemble_tiles_device(local_rank, WIDTH, HEIGHT, TILE, TILE, self.plan.frames, world, gathered.data_ptr(),
-                                    gathered.numel(), out.data_ptr(), out.numel(), stream.cuda_stream)
+                                    gathered.numel(), out.data_ptr(), out.numel(), self.side.cuda_stream)
             return out.view(self.plan.frames, HEIGHT, WIDTH, 3)
 
         def step(self, i):
