@@ -89,3 +89,19 @@ def test_comm_id_without_gpu_and_init_refusal():
         with pytest.raises(R.RtError) as ei:
             R.Comm(0, 0, 1, a)
         assert ei.value.code == _capi.RT_E_NODEV
+
+
+def test_tune_knobs_validate_ranges(tmp_path):
+    """rt_scene_tune range checks on a host-only scene (no GPU): the launch-shape knobs accept
+    their documented values and refuse others with RT_E_ARG."""
+    p = tmp_path / "t.obj"
+    p.write_text("v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 3\n")
+    s = R.Scene.load(str(p), device=R.RT_HOST_ONLY)
+    for knob, good, bad in [("wave_steal", (0, 1, 2), (-1, 3)), ("chain_refill", (0, 1), ()),
+                            ("refill_grid", (1, 2560), (0, 70000)), ("batch_order", (0, 1, 2), (3,)),
+                            ("chain_split", (0, 3, 7), (8,)), ("pipes", (1, 4), (0, 5))]:
+        for v in good:
+            s.tune(knob, v)
+        for v in bad:
+            with pytest.raises(R.RtError):
+                s.tune(knob, v)
