@@ -34,6 +34,8 @@ FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector (= FP32 matrix)
 # The same issue rate without packing (x2) or FMA (x2), which parity forbids for the triangle test:
 # 256 CUs x 64 lanes x 2.4 GHz x 1 flop = 39.3 TFLOP/s (the brute-force kernel's practical ceiling)
 FP32_NOFMA_NOPACK_TFLOPS = 39.3
+VALU_CYCLES_PER_WAVE_INST = 4   # wave64 non-packed FP32 op on one SIMD (tools/valu_rate.hip: 38.7 T lane-ops/s)
+CLOCK_HZ = 2.4e9
 HBM_PEAK_GBS = 8000.0
 TILE = 16
 # BASELINE.json configs. C4 is the metric's configuration and the default; the
@@ -421,8 +423,22 @@ def main():
         avg_s = ch_ms / 1e3 / max(ch_launches, 1)
         achieved = flops / max(ch_launches, 1) / avg_s / 1e12 if avg_s > 0 else 0.0
         # the committed PMC summary profiles the default workload (C4): other workloads carry none
+        issue = None
         if args.workload == "c4" and args.accel == "bvh":
             traffic, traffic_src = pmc_traffic(kname)
+            pc, pc_src = pmc_counters(kname, "SQ_THREAD_CYCLES_VALU_per_launch")
+            if pc and avg_s > 0 and pc.get("SQ_INSTS_VALU_per_launch") and pc.get("SQ_ACTIVE_INST_VALU_per_launch"):
+                simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+                iv = pc["SQ_INSTS_VALU_per_launch"]
+                issue = {"valu_wave_instructions_per_launch": round(iv),
+                         "valu_busy_frac": round(iv * VALU_CYCLES_PER_WAVE_INST / (simds * avg_s * CLOCK_HZ), 3),
+                         "lane_utilization": round(pc["SQ_THREAD_CYCLES_VALU_per_launch"] /
+                                                   (64.0 * pc["SQ_ACTIVE_INST_VALU_per_launch"]), 3),
+                         "source": pc_src,
+                         "what": "VALU issue roof: wave-instructions x 4 cycles (wave64, non-packed, "
+                                 "profiles/r02_valu_rate.txt) / (SIMDs x launch time x 2.4 GHz); lane_utilization = "
+                                 "SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU), the share of lanes active "
+                                 "per issued VALU instruction"}
         dram = None
         if traffic and avg_s > 0:
             dram = {"achieved": round(traffic / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -481,6 +497,7 @@ def main():
                 "avg_launch_ms": round(avg_s * 1e3, 4),
                 "timing": "HIP events on the launch stream, batch-ordered launches of the timed entry point only",
                 "dram": dram,
+                "issue": issue,
                 "logical_bytes_per_launch": round(logical / max(ch_launches, 1)),
                 "logical_bytes_what": "L1-side accesses (64 B per node visit and per triangle test, 32 B per query "
                                       "in and per chain record out); most are served by L1/L2, so this is not HBM traffic",
@@ -519,6 +536,13 @@ def main():
 def pmc_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*_pmc.json,
     written by tools/pmc_summary.py from separate rocprofv3 --pmc passes of this bench command)."""
+    c, src = pmc_counters(kernel, "traffic_bytes_per_launch")
+    return (c["traffic_bytes_per_launch"], src) if c else (None, None)
+
+
+def pmc_counters(kernel: str, need: str):
+    """The per-launch counters of `kernel` (its timed instantiation) from the newest committed PMC
+    summary that has counter `need`: (dict, file) or (None, None)."""
     import glob
     files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc.json")))   # round-tagged names sort by age
     for f in reversed(files):
@@ -535,8 +559,8 @@ def pmc_traffic(kernel: str):
         names = [n for n in ks if n == kernel or (n.startswith(kernel + "<") and counting(n) == "false")]
         names.sort(key=lambda n: -ks[n].get("launches_in_pass", 0))
         for n in names:
-            if "traffic_bytes_per_launch" in ks[n]:
-                return ks[n]["traffic_bytes_per_launch"], os.path.relpath(f, HERE)
+            if need in ks[n]:
+                return ks[n], os.path.relpath(f, HERE)
     return None, None
 
 
