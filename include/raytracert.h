@@ -284,6 +284,11 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
                                     and later ones use the faster (before that: on when the launch is at
                                     most two rounds of resident waves). C2 0.24 -> 0.18 ms, C3 -4%;
                                     C4 is faster without */
+#define RT_TUNE_STEAL_HALF 22    /* ordered launches of the stealing kernel: at most this many of the longest
+                                    batches (and at most 1/32 of them) run as two waves of 32 samples, the
+                                    other 32 lanes of each starting as helpers (default 512; 0 off) */
+#define RT_TUNE_STEAL_QUARTER 23 /* ... and before them this many of the longest run as four waves of 16
+                                    samples each (48 helpers per wave; default 0) */
 #define RT_TUNE_TOP_NODES 13     /* four-wide nodes of the tree's top levels (breadth-first, the first
                                     ones in the node array) each block reads from an LDS copy (0-85) */
 #define RT_TUNE_CHAIN_SPLIT 12   /* query distribution of the chain launch: as RT_TUNE_XCD_SPLIT, or 3: 64-query

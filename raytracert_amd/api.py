@@ -269,7 +269,8 @@ class Scene:
              "batch_order": _capi.TUNE_BATCH_ORDER,
              "order_every": _capi.TUNE_ORDER_EVERY, "fuse_pixels": _capi.TUNE_FUSE_PIXELS,
              "chain_refill": _capi.TUNE_CHAIN_REFILL, "refill_grid": _capi.TUNE_REFILL_GRID,
-             "wave_steal": _capi.TUNE_WAVE_STEAL}[knob]
+             "wave_steal": _capi.TUNE_WAVE_STEAL, "steal_half": _capi.TUNE_STEAL_HALF,
+             "steal_quarter": _capi.TUNE_STEAL_QUARTER}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
 
     def bvh_digest(self) -> int:

@@ -89,6 +89,8 @@ struct DevScene {
     int32_t chain_refill;           // RT_TUNE_CHAIN_REFILL: per-lane pixel refill in the chain launch
     int32_t wave_steal;             // RT_TUNE_WAVE_STEAL: 0 off, 1 on, 2 when the chain launch is <= 2 wave rounds
     int32_t refill_grid;            // its (resident) grid, blocks of 128 threads
+    int32_t steal_half;             // RT_TUNE_STEAL_HALF: half-wave batches of the ordered stealing launch
+    int32_t steal_quarter;          // RT_TUNE_STEAL_QUARTER: quarter-wave batches before them
 };
 
 struct DevWork {

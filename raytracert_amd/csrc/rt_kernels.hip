@@ -913,9 +913,7 @@ __device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, 
 #ifndef RT_STEAL_MIN_IDLE
 #define RT_STEAL_MIN_IDLE 8   // steal only when at least this many lanes of the wave are idle
 #endif
-#ifndef RT_STEAL_SPLIT
-#define RT_STEAL_SPLIT 512   // at most this many of the longest batches run as two half waves (k_chain)
-#endif
+// (how many of the longest batches run as half or quarter waves: RT_TUNE_STEAL_HALF / _QUARTER)
 #ifndef RT_STEAL_SPLIT_DIV
 #define RT_STEAL_SPLIT_DIV 32   // ... and at most this fraction (1 / DIV) of them
 #endif
@@ -2132,18 +2130,22 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
 #endif
     const int nq = kInlinePrimary ? static_cast<int>(static_cast<int64_t>(g.ntiles) * g.tw * g.th * g.pfx * g.pfy)
                                   : w.counters[first];
-    // split (ordered launches of the stealing kernel): the first `split` batches of the order (the
-    // longest) run as two waves of 32 samples each, so the other 32 lanes of each are free to
-    // steal subtrees of the long walks from the start; virtual wave vb < 2 * split is half vb & 1
-    // of batch order[vb >> 1], later ones batch order[vb - split]
-    drive_queries(nq + split * kWave, sc.chain_split & 3, w.wq + (2 * first) * kWqSlot, [&](int j0, int vend) {
-        const int end = vend - split * kWave;
+    // split (ordered launches of the stealing kernel) = s2 | s4 << 16: the first s4 batches of the
+    // order (the longest) run as four waves of 16 samples each, the next s2 as two waves of 32, so
+    // the other lanes of each are free to steal subtrees of the long walks from the start. Virtual
+    // wave vb < 4 * s4 is quarter vb & 3 of batch order[vb >> 2]; then vb - 4 * s4 < 2 * s2 is half
+    // (vb - 4 * s4) & 1 of batch order[s4 + ((vb - 4 * s4) >> 1)]; later ones batch order[vb - extra]
+    const int s2 = split & 0xFFFF, s4 = split >> 16, extra = 3 * s4 + s2;
+    drive_queries(nq + extra * kWave, sc.chain_split & 3, w.wq + (2 * first) * kWqSlot, [&](int j0, int vend) {
+        const int end = vend - extra * kWave;
         const int vb = j0 >> 6;   // this wave's batch in dispatch order (wave-uniform when ordered)
-        const bool half = ordered && vb < 2 * split;
-        const int ob = half ? (vb >> 1) : vb - (ordered ? split : 0);
+        const bool quarter = ordered && vb < 4 * s4;
+        const bool half = ordered && !quarter && vb - 4 * s4 < 2 * s2;
+        const int ob = quarter ? (vb >> 2) : half ? s4 + ((vb - 4 * s4) >> 1) : vb - (ordered ? extra : 0);
         const int pb = (ordered && (vb << 6) < vend) ? w.batch_order[ob] : vb;
-        const int lane_off = half ? ((vb & 1) * (kWave / 2) + __lane_id()) : (j0 & (kWave - 1));
-        const bool lane_on = !half || __lane_id() < kWave / 2;
+        const int lane_off = quarter ? ((vb & 3) * (kWave / 4) + __lane_id())
+                           : half    ? (((vb - 4 * s4) & 1) * (kWave / 2) + __lane_id()) : (j0 & (kWave - 1));
+        const bool lane_on = quarter ? __lane_id() < kWave / 4 : !half || __lane_id() < kWave / 2;
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         V3 rgb = mk(0, 0, 0);   // fused pixels: this lane's folded chain and its pixel (valid samples)
         int px = -1;
@@ -2519,22 +2521,33 @@ __global__ __launch_bounds__(kBlock) void k_ray_triangle_pairs(const float *__re
 }
 
 // Un-permute of gathered tile shards (multi-GPU frame): gathered = [rank][slot]
-// tiles of tw x th x 3 bytes, global tile id g = f * T + t held by rank g % N in slot g / N; one
-// thread per output pixel of frames x height x width (row-major, 3 bytes each).
+// tiles of tw x th x 3 bytes, global tile id g = f * T + t held by rank g % N in slot g / N. One
+// thread per row of a gathered tile: it copies the row's (clipped) tw x 3 bytes to the frame, in
+// 16-B pieces when both ends are 16-B aligned (tw = 16 at 1920 wide: always). Index math per tile
+// row, not per byte (the per-pixel form's 64-bit divisions cost ~20 us per C4 frame).
 __global__ __launch_bounds__(kBlock) void k_assemble_tiles(const uint8_t *__restrict__ gathered, int32_t width,
                                                            int32_t height, int32_t tw, int32_t th, int32_t tiles_x,
                                                            int32_t tiles_total, int32_t nranks, int64_t slots,
-                                                           int64_t npix, uint8_t *__restrict__ out) {
+                                                           int32_t frames, uint8_t *__restrict__ out) {
     const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (i >= npix) return;
-    const int64_t per_frame = static_cast<int64_t>(width) * height;
-    const int64_t f = i / per_frame, q = i - f * per_frame;
-    const int y = static_cast<int>(q / width), x = static_cast<int>(q - static_cast<int64_t>(y) * width);
-    const int64_t g = f * tiles_total + static_cast<int64_t>(y / th) * tiles_x + x / tw;
-    const int64_t tile = (g % nranks) * slots + g / nranks;
-    const uint8_t *src = gathered + (tile * tw * th + static_cast<int64_t>(y % th) * tw + x % tw) * 3;
-    uint8_t *dst = out + 3 * i;
-    dst[0] = src[0]; dst[1] = src[1]; dst[2] = src[2];
+    const int64_t tile = i / th;   // gathered tile (rank-major), row r of it
+    const int r = static_cast<int>(i - tile * th);
+    if (tile >= nranks * slots) return;
+    const int64_t rank = tile / slots, slot = tile - rank * slots;
+    const int64_t g = slot * nranks + rank;   // < 2^30 (rt_render_tiles_device's bound)
+    if (g >= static_cast<int64_t>(frames) * tiles_total) return;   // a padding slot
+    const int f = static_cast<int>(g / tiles_total), t = static_cast<int>(g - static_cast<int64_t>(f) * tiles_total);
+    const int ty = t / tiles_x, tx = t - ty * tiles_x;
+    const int y = ty * th + r, x0 = tx * tw;
+    if (y >= height) return;
+    const int n = min(tw, width - x0) * 3;
+    const uint8_t *src = gathered + (tile * tw * th + static_cast<int64_t>(r) * tw) * 3;
+    uint8_t *dst = out + ((static_cast<int64_t>(f) * height + y) * width + x0) * 3;
+    int k = 0;
+    if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0)
+        for (; k + 16 <= n; k += 16)
+            *reinterpret_cast<uint4 *>(dst + k) = *reinterpret_cast<const uint4 *>(src + k);
+    for (; k < n; ++k) dst[k] = src[k];
 }
 
 inline unsigned grid_for(int64_t n) { return static_cast<unsigned>((n + kBlock - 1) / kBlock); }
@@ -2714,10 +2727,16 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
                            s.leaf_idx, out_u8, out_f32, geom);
         return;
     }
-    // the stealing kernel, ordered over grid-stride batches: the longest batches run as half waves
-    const int split = (steal && ordered && (s.chain_split & 7) == 0 && RT_STEAL_SPLIT > 0)
-                          ? static_cast<int>(std::min<int64_t>((capacity + kWave - 1) / kWave / RT_STEAL_SPLIT_DIV, RT_STEAL_SPLIT)) : 0;
-    hipLaunchKernelGGL(k, dim3(grid_bvh(capacity + static_cast<int64_t>(split) * kWave, s.bvh_grid)), dim3(kBvhBlock),
+    // the stealing kernel, ordered over grid-stride batches: the longest batches run as quarter and
+    // half waves (at most 1/RT_STEAL_SPLIT_DIV of the batches together)
+    int s2 = 0, s4 = 0;
+    if (steal && ordered && (s.chain_split & 7) == 0) {
+        const int64_t cap = (capacity + kWave - 1) / kWave / RT_STEAL_SPLIT_DIV;
+        s4 = static_cast<int>(std::min<int64_t>(cap, s.steal_quarter));
+        s2 = static_cast<int>(std::min<int64_t>(cap - s4, s.steal_half));
+    }
+    const int split = s2 | (s4 << 16);
+    hipLaunchKernelGGL(k, dim3(grid_bvh(capacity + static_cast<int64_t>(3 * s4 + s2) * kWave, s.bvh_grid)), dim3(kBvhBlock),
                        bvh_lds(s), stream, s, p, w, first, s.nodes4, s.leaf_recs, s.leaf_idx, ordered ? 1 : 0, out_u8,
                        out_f32, fuse_spp, geom, split);
 }
@@ -2782,10 +2801,10 @@ void launch_assemble_tiles(const uint8_t *gathered, int32_t width, int32_t heigh
                            int32_t nranks, uint8_t *out, hipStream_t stream) {
     const int32_t tiles_x = (width + tw - 1) / tw, tiles_total = tiles_x * ((height + th - 1) / th);
     const int64_t slots = (static_cast<int64_t>(frames) * tiles_total + nranks - 1) / nranks;
-    const int64_t npix = static_cast<int64_t>(frames) * width * height;
-    if (npix <= 0) return;
-    hipLaunchKernelGGL(k_assemble_tiles, dim3(static_cast<unsigned>((npix + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
-                       gathered, width, height, tw, th, tiles_x, tiles_total, nranks, slots, npix, out);
+    const int64_t rows = static_cast<int64_t>(nranks) * slots * th;   // one thread per gathered tile row
+    if (rows <= 0 || static_cast<int64_t>(frames) * width * height <= 0) return;
+    hipLaunchKernelGGL(k_assemble_tiles, dim3(static_cast<unsigned>((rows + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                       gathered, width, height, tw, th, tiles_x, tiles_total, nranks, slots, frames, out);
 }
 
 }  // namespace rt

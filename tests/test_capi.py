@@ -99,7 +99,9 @@ def test_tune_knobs_validate_ranges(tmp_path):
     s = R.Scene.load(str(p), device=R.RT_HOST_ONLY)
     for knob, good, bad in [("wave_steal", (0, 1, 2), (-1, 3)), ("chain_refill", (0, 1), ()),
                             ("refill_grid", (1, 2560), (0, 70000)), ("batch_order", (0, 1, 2), (3,)),
-                            ("chain_split", (0, 3, 7), (8,)), ("pipes", (1, 4), (0, 5))]:
+                            ("chain_split", (0, 3, 7), (8,)),
+                            ("steal_half", (0, 512, 65535), (-1, 65536)), ("steal_quarter", (0, 8, 4096), (-1, 4097)),
+                            ("pipes", (1, 4), (0, 5))]:
         for v in good:
             s.tune(knob, v)
         for v in bad:

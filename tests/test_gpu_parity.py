@@ -422,6 +422,27 @@ def test_wave_steal_matches_plain_walk(spec, w, h, pf, lights, workdir, gpu_avai
             assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
 
 
+@pytest.mark.parametrize("spec,w,h,pf,half,quarter", [("ref:dodgeColorTest.obj", 400, 300, 1, 512, 8),
+                                                        ("ref:dodgeColorTest.obj", 200, 150, 1, 0, 4096),
+                                                        ("syn:C4", 160, 90, 2, 3, 5), ("syn:F4", 96, 54, 4, 0, 2)])
+def test_steal_split_matches_plain_walk(spec, w, h, pf, half, quarter, workdir, gpu_available):
+    """RT_TUNE_STEAL_HALF / RT_TUNE_STEAL_QUARTER: in ordered launches of the stealing kernel the
+    longest batches run as four waves of 16 samples and the next as two of 32 (pf 2 and 4: a
+    pixel's sub-samples stay in adjacent lanes of one part). Frames, floats and ray counts equal the
+    plain walk's on every launch (the first is unordered, later ones ordered)."""
+    p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
+    with R.Scene.load(scene_path(spec, workdir), device=0) as sc:
+        sc.tune("wave_steal", 0)
+        ref, reff, refc = sc.render(p, want_f32=True)
+        sc.tune("wave_steal", 1)
+        sc.tune("steal_half", half)
+        sc.tune("steal_quarter", quarter)
+        for _ in range(4):
+            u8, f32, c = sc.render(p, want_f32=True)
+            assert [int(x) for x in c] == [int(x) for x in refc]
+            assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
+
+
 def test_wave_steal_auto_trials_keep_results(workdir, gpu_available):
     """RT_TUNE_WAVE_STEAL 2 (default): launches 2 and 3 over a frame geometry are timed without and
     with stealing, later ones use the faster; every render of the sequence equals the plain walk's."""
