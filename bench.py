@@ -105,31 +105,10 @@ def parse():
     ap.add_argument("--accel", choices=("bvh", "brute_force"), default="bvh")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c4")
     ap.add_argument("--no-bf-roofline", action="store_true", help="skip the brute-force kernel's roofline frame")
-    ap.add_argument("--prof-timed-only", action="store_true",
-                    help="roctxProfilerResume/Pause around the timed region (rocprofv3 --selected-regions)")
     ap.add_argument("--pipes", type=int, default=1, help="render pipelines a call's batches overlap on")
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
                     help="extra launch-shape knob (Scene.tune), e.g. shadow_virtual=-1; repeatable")
     return ap.parse_args()
-
-
-_ROCTX = []
-
-
-def prof_region(on):
-    """--prof-timed-only: under `rocprofv3 --selected-regions` only the timed frames are traced, so
-    the profile's kernel averages cover the same launches as ms_per_step (no warm-up launches)."""
-    if not ARGS_PROF[0]:
-        return
-    if not _ROCTX:
-        import ctypes
-        lib = ctypes.CDLL("/opt/rocm/lib/libroctx64.so.4")   # (torch bundles an older one without these)
-        lib.roctxProfilerResume.argtypes = lib.roctxProfilerPause.argtypes = [ctypes.c_uint64]
-        _ROCTX.append(lib)
-    (_ROCTX[0].roctxProfilerResume if on else _ROCTX[0].roctxProfilerPause)(0)
-
-
-ARGS_PROF = [False]
 
 
 def log(*a):
@@ -138,7 +117,6 @@ def log(*a):
 
 def main():
     args = parse()
-    ARGS_PROF[0] = args.prof_timed_only
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -298,7 +276,6 @@ def main():
             if world > 1:
                 dist.barrier()
             torch.cuda.synchronize(dev)
-            prof_region(True)
             t0 = time.perf_counter()
             frames = None
             for i in range(steps):
@@ -307,7 +284,6 @@ def main():
             f = self.drain()   # the last step's gather + un-permute stay inside the timed region
             frames = f if f is not None else frames
             torch.cuda.synchronize(dev)
-            prof_region(False)
             if world > 1:
                 dist.barrier()
             el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
@@ -326,8 +302,8 @@ def main():
     rays_per_step = float(ct.sum().item())
     rays_by_kind = [int(x) for x in ct.tolist()]
 
+    # ---- timed region (the metric) ----
     elapsed, frames = main_run.run(args.steps, args.warmup)
-    ARGS_PROF[0] = False   # only the main timed region is traced under --prof-timed-only
 
     rehearsal = None
     if args.rehearse and rank == 0 and frames is not None:   # every assembled frame = the one-GPU frame
