@@ -103,6 +103,7 @@ struct DevWork {
     float4 *chain_coef;             // [step][sample]: xyz = coefficient on the child's colour
     uint8_t *depth;                 // per sample: number of chain steps
     int32_t *counters;              // [step] main queue sizes (step 0 dense, incl. inactive), [kMaxStepsCounters + step] shadow
+    int32_t *counters_next;         // in-lane fused chain launch: the next launch's counters, zeroed by this one (or null)
     int32_t *wq;                    // [2 * step + shadow] work-queue slots of kWqSlot ints (RT_TUNE_XCD_SPLIT 2)
     int32_t *pix_out;               // per sample (fused pixel writes): its pixel's output index
     uint32_t *batch_cost;           // chain launch: per 64-sample batch, its wave's duration (100 MHz ticks)

@@ -2130,6 +2130,11 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
 #endif
     const int nq = kInlinePrimary ? static_cast<int>(static_cast<int64_t>(g.ntiles) * g.tw * g.th * g.pfx * g.pfy)
                                   : w.counters[first];
+    if (kInlinePrimary && w.counters_next) {   // k_gen_primary's resets, for the next launch (Pipe::cnt_buf)
+        const int i0 = blockIdx.x * kBvhBlock + threadIdx.x;   // (this launch's counters: already zero)
+        for (int i = i0; i < 2 * kMaxStepsCounters; i += gridDim.x * kBvhBlock) w.counters_next[i] = 0;
+        if (i0 == 0) w.counters[0] = nq;
+    }
     // split (ordered launches of the stealing kernel) = s2 | s4 << 16: the first s4 batches of the
     // order (the longest) run as four waves of 16 samples each, the next s2 as two waves of 32, so
     // the other lanes of each are free to steal subtrees of the long walks from the start. Virtual
