@@ -247,7 +247,7 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
 /* ---- tuning (launch-shape knobs; results never depend on them) ------------------------- */
 #define RT_TUNE_XCD_SPLIT 0   /* BVH queue distribution: 0 grid-stride, 1 one static segment per XCD,
                                  2 per-XCD segments with work-stealing wave counters */
-#define RT_TUNE_BVH_GRID  1   /* grid cap (blocks of 128 threads) of the BVH kernels; default 16384: the
+#define RT_TUNE_BVH_GRID  1   /* grid cap (blocks of 256 threads) of the BVH kernels; default 16384: the
                                  chain launch then gives each wave one 64-sample batch of a C4 frame
                                  and the dispatcher balances the blocks */
 #define RT_TUNE_BVH_WIDTH 2   /* 4 (default): quantised four-wide nodes; 2: float binary nodes */
@@ -275,7 +275,7 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
                                     work counters), so lanes do not wait for a batch's longest chain;
                                     0 (default): fixed 64-sample batches with the batch order (measured
                                     faster: a wave's rays then share a chain step and stay coherent) */
-#define RT_TUNE_REFILL_GRID 20   /* blocks (of 128 threads) of the refill chain launch (default: resident,
+#define RT_TUNE_REFILL_GRID 20   /* blocks (of 256 threads) of the refill chain launch (default: resident,
                                     10 per CU) */
 #define RT_TUNE_WAVE_STEAL 21    /* in-wave work stealing in the chain launch: a lane whose query is done
                                     walks a subtree from another lane's stack with that lane's ray

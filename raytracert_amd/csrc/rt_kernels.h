@@ -88,7 +88,7 @@ struct DevScene {
     int32_t top_nodes;              // RT_TUNE_TOP_NODES: four-wide nodes [0, top_nodes) read from an LDS copy
     int32_t chain_refill;           // RT_TUNE_CHAIN_REFILL: per-lane pixel refill in the chain launch
     int32_t wave_steal;             // RT_TUNE_WAVE_STEAL: 0 off, 1 on, 2 when the chain launch is <= 2 wave rounds
-    int32_t refill_grid;            // its (resident) grid, blocks of 128 threads
+    int32_t refill_grid;            // its (resident) grid, blocks of kBvhBlock (RT_BVH_BLOCK) threads
     int32_t steal_half;             // RT_TUNE_STEAL_HALF: half-wave batches of the ordered stealing launch
     int32_t steal_quarter;          // RT_TUNE_STEAL_QUARTER: quarter-wave batches before them
 };
@@ -138,8 +138,9 @@ void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *
 // k_frame's arithmetic, so no k_frame follows.
 // g (fused launches from step 0): the batch's frame geometry; in-lane chain kernels then make their
 // primary rays themselves (launch_gen_primary(fused) only resets the counters; primaries_inline()).
-// blocks of 128 threads of the chain kernels resident per CU (4 SIMDs x waves per EU / 2)
+// blocks of the chain kernels resident per CU (4 SIMDs x waves per EU x 64 / block threads)
 int chain_blocks_per_cu();
+int bvh_block_threads();   // threads per block of the BVH and chain kernels (RT_BVH_BLOCK)
 // whether launch_chain runs the per-lane refill kernel (k_chain_refill) for these arguments
 bool chain_refill_used(const DevScene &s, int fuse_spp, const FrameGeom *g);
 void launch_chain(const DevScene &s, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,

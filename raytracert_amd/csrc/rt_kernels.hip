@@ -207,7 +207,11 @@ __device__ __forceinline__ void closest_hit_loop(const TriRec *__restrict__ tris
 // its padded box misses the ray or (closest-hit) when even its entry point is farther than the
 // current best. Leaves run test_triangle on the leaf-ordered records with the original index.
 // ---------------------------------------------------------------------------------------------
-constexpr int kBvhBlock = 128;
+#ifndef RT_BVH_BLOCK
+#define RT_BVH_BLOCK 256   // threads per block of the BVH and chain kernels (r02h: 256 vs 128 measured C4 0.44 vs
+                           // 0.48 ms, C3 0.250 vs 0.259, C5 8.75 vs 8.91; C2 0.178 vs 0.171; 64: C4 0.61 ms)
+#endif
+constexpr int kBvhBlock = RT_BVH_BLOCK;
 #ifndef RT_SORT_ANYHIT
 #define RT_SORT_ANYHIT 0
 #endif
@@ -2747,6 +2751,7 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
 }
 
 int chain_blocks_per_cu() { return 4 * RT_CHAIN_WPE * kWave / kBvhBlock; }
+int bvh_block_threads() { return kBvhBlock; }
 
 bool chain_refill_used(const DevScene &s, int fuse_spp, const FrameGeom *g) {
     return RT_CHAIN_INLANE && primaries_inline() && s.chain_refill && s.refill_grid > 0 && fuse_spp > 0 && g != nullptr &&
