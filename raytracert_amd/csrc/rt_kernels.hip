@@ -2401,15 +2401,14 @@ __device__ __forceinline__ int order_bucket(uint32_t c) {
     return kOrderBuckets - 1 - min(k, kOrderBuckets - 1);   // descending duration
 }
 
-// XCD segments (segs == kXcds): dispatch slot v runs on XCD (v / W) % 8 (W = kBvhBlock / 64 wave
-// batches per block, blocks dealt round-robin to the XCDs), so XCD x owns seg_count(n, x) of the n slots.
+// XCD segments (segs == kXcds): dispatch slot v runs on XCD (v / 2) % 8 (two wave batches per
+// block, blocks dealt round-robin to the XCDs), so XCD x owns seg_count(n, x) of the n slots. (Measured
+// with 128-thread blocks; with 256 the segments are placement hints only, and the ordered launch's
+// batch mapping depends on this exact count, so it stays as measured.)
 // Segment x is that many consecutive batches in screen order and the sort runs within each
 // segment: each XCD's L2 then holds the geometry of one band of the screen, and within the band
 // the longest batches go first. Placement only; results never change.
-__device__ __forceinline__ int seg_count(int n, int x) {
-    constexpr int W = kBvhBlock / kWave;
-    return W * (n / (kXcds * W)) + min(W, max(0, n % (kXcds * W) - W * x));
-}
+__device__ __forceinline__ int seg_count(int n, int x) { return 2 * (n / 16) + min(2, max(0, n % 16 - 2 * x)); }
 __device__ __forceinline__ int seg_of(int n, int i, int &start) {
     int x = 0;
     start = 0;
