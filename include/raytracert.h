@@ -254,29 +254,23 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
 #define RT_TUNE_LDS_STACK 3   /* traversal stack entries per lane kept in LDS; deeper ones in HBM */
 #define RT_TUNE_PIPES     4   /* 1-4 render pipelines (workspace + stream) a call's batches overlap on
                                  (default 1) */
-#define RT_TUNE_WAVE_TRAVERSAL 8   /* bit k: closest-hit of chain step k, bit 16+k: its shadow rays,
-                                      bit 31: rt_intersect_mesh, walk the four-wide tree once per
-                                      wave (coherent rays); default 0: measured no faster on C4,
-                                      primaries included (VALU-bound, not fetch-bound) */
+#define RT_TUNE_WAVE_TRAVERSAL 8   /* retired in r03 (only 0 accepted): the wave-coherent walk of the
+                                      four-wide tree measured no faster on C4, primaries included */
 #define RT_TUNE_CHAIN_FROM 9     /* chain steps from this one on run in one launch, each lane carrying
                                     its ray through closest-hit, shadows and shade (default 0;
                                     >= max_lvl + 1: every step its own launches) */
-#define RT_TUNE_BATCH_ORDER 15  /* 1 (default): the chain launch dispatches its 64-sample batches longest
+#define RT_TUNE_BATCH_ORDER 15  /* 1 (default): the chain launch dispatches its wave batches longest
                                     first, by the durations the pipeline's previous launch over the
                                     same batches measured (the first launch runs in screen order);
-                                    2: the same within eight screen bands, one per XCD (L2 locality) */
+                                    0: screen order */
 #define RT_TUNE_ORDER_EVERY 17  /* batch order re-sorted every this many launches over the same batches
                                     (default 8; 1: every launch); the durations are measured every time */
 #define RT_TUNE_FUSE_PIXELS 18  /* 1 (default): the chain launch writes each pixel when its samples'
-                                    chains end (no separate frame pass) when pf*pf divides 64;
-                                    0: always the frame pass */
-#define RT_TUNE_CHAIN_REFILL 19  /* 1: in the chain launch each lane owns one pixel at a time, runs its
-                                    sub-samples' chains in order and then takes the next pixel (per-XCD
-                                    work counters), so lanes do not wait for a batch's longest chain;
-                                    0 (default): fixed 64-sample batches with the batch order (measured
-                                    faster: a wave's rays then share a chain step and stay coherent) */
-#define RT_TUNE_REFILL_GRID 20   /* blocks (of 256 threads) of the refill chain launch (default: resident,
-                                    10 per CU) */
+                                    chains end (no separate frame pass) when pfx*pfy <= 64 (a wave
+                                    batch holds floor(64 / spp) whole pixels); 0: always the frame pass */
+#define RT_TUNE_CHAIN_REFILL 19  /* retired in r03 (only 0 accepted): per-lane pixel refill measured 1.5x
+                                    slower on C4 (a wave's rays lose their shared chain step) */
+#define RT_TUNE_REFILL_GRID 20   /* retired in r03 with it (only 0 accepted) */
 #define RT_TUNE_WAVE_STEAL 21    /* in-wave work stealing in the chain launch: a lane whose query is done
                                     walks a subtree from another lane's stack with that lane's ray
                                     (four-wide tree). 0 off, 1 on, 2 (default, auto): the second and
@@ -286,14 +280,15 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
                                     C4 is faster without */
 #define RT_TUNE_STEAL_HALF 22    /* ordered launches of the stealing kernel: at most this many of the longest
                                     batches (and at most 1/32 of them) run as two waves of 32 samples, the
-                                    other 32 lanes of each starting as helpers (default 512; 0 off) */
+                                    other 32 lanes of each starting as helpers (default 512; 0 off; only
+                                    when 32 lanes hold whole pixels, i.e. pfx*pfy divides 32) */
 #define RT_TUNE_STEAL_QUARTER 23 /* ... and before them this many of the longest run as four waves of 16
-                                    samples each (48 helpers per wave; default 0) */
+                                    samples each (48 helpers per wave; default 0; pfx*pfy divides 16) */
 #define RT_TUNE_TOP_NODES 13     /* four-wide nodes of the tree's top levels (breadth-first, the first
                                     ones in the node array) each block reads from an LDS copy (0-85) */
 #define RT_TUNE_CHAIN_SPLIT 12   /* query distribution of the chain launch: as RT_TUNE_XCD_SPLIT, or 3: 64-query
                                     chunks dealt round-robin to the XCDs and taken dynamically within
-                                    each (+4: reversed order, diagnostic) */
+                                    each */
 #define RT_TUNE_PIPE_BATCHES 6     /* split a call into at least pipes x this many batches */
 #define RT_TUNE_PIPE_PRIORITY 7    /* 1 (default): pipelines after the first run at lower stream priority */
 #define RT_TUNE_SHADOW_VIRTUAL 5   /* bit k: step k's shadow rays are read from its hits directly
@@ -331,10 +326,18 @@ int rt_work_stats(rt_scene *scene, int32_t kind, double *tests, double *node_vis
  * tasks, [5] sum over wave tasks of the largest per-query test count. */
 #define RT_WORK_FIELDS 6
 int rt_work_detail(rt_scene *scene, int32_t kind, uint64_t out[RT_WORK_FIELDS]);
-/* Diagnostic words written by diagnostic kernel builds (e.g. -DRT_WAVE_TIMES: per-wave start and
- * end clocks of the chain launch) while profiling is RT_PROFILE_WORK; 0 in production builds.
+/* Diagnostic words reserved for diagnostic kernel builds (none in r03: the wave-time, region-count
+ * and stamp builds were retired with the variants they measured); 0 in production builds.
  * Reads count words from offset (offset + count <= 131072); synchronises the device. */
 int rt_diag_read(rt_scene *scene, int64_t offset, int64_t count, uint64_t *out);
+/* The render workspace of one pipeline for `cap` samples, `steps` = max_lvl + 1 chain steps and
+ * `lights` lights, as the library carves it (no allocation, no device): total bytes and, per array
+ * in carving order, (offset, bytes): q_org[0], q_dst[0], q_org[1], q_dst[1], hit_idx, hit_I, sq_org,
+ * sq_dst, shadow, chain_local, chain_coef, depth, counters[0], counters[1], wq, cost[0], order[0],
+ * cost[1], order[1], order_scratch. For tests of the sizing. */
+#define RT_WS_ARRAYS 20
+int rt_workspace_layout(int64_t cap, int32_t steps, int32_t lights, uint64_t *total_bytes,
+                        uint64_t extents[2 * RT_WS_ARRAYS]);
 
 #ifdef __cplusplus
 }

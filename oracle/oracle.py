@@ -88,9 +88,9 @@ class OraDebugBounce(C.Structure):
 
 
 def make_params(width, height, pf=1, max_lvl=0, lights=((0.0, 0.0, 4.0),), flags=ALL_FEATURES,
-                camera_pos=(0.0, 0.0, 4.0), corners=None, seed=DEFAULT_SEED) -> OraParams:
+                camera_pos=(0.0, 0.0, 4.0), corners=None, seed=DEFAULT_SEED, pfy=None) -> OraParams:
     p = OraParams()
-    p.width, p.height, p.pfx, p.pfy = width, height, pf, pf
+    p.width, p.height, p.pfx, p.pfy = width, height, pf, pf if pfy is None else pfy
     p.max_lvl, p.flags, p.n_lights = max_lvl, flags, len(lights)
     p.seed = seed
     for i, l in enumerate(lights):

@@ -25,6 +25,7 @@ RT_E_RCCL = -7
 COMM_ID_BYTES = 128
 RT_HOST_ONLY = -1
 RT_MAX_LIGHTS = 16
+RT_WS_ARRAYS = 20   # rt_workspace_layout arrays
 
 AMBIENT, DIFFUSE, SPECULAR, REFLECTION, SHADOWS, REFRACTION = (1 << i for i in range(6))
 ALL_FEATURES = 0x3F
@@ -109,6 +110,7 @@ _SIGNATURES = {
     "rt_scene_bvh_info": ([_VP, _VP], C.c_int),
     "rt_work_detail": ([_VP, C.c_int32, _VP], C.c_int),
     "rt_diag_read": ([_VP, C.c_int64, C.c_int64, _VP], C.c_int),
+    "rt_workspace_layout": ([C.c_int64, C.c_int32, C.c_int32, C.POINTER(C.c_uint64), _VP], C.c_int),
     "rt_scene_bvh_digest": ([_VP, C.POINTER(C.c_uint64)], C.c_int),
     "rt_scene_bvh_validate": ([_VP], C.c_int),
     "rt_bvh_acceptance_box": ([_VP, _VP, _VP], C.c_int),

@@ -51,12 +51,13 @@ class RenderParams:
     camera_pos: Sequence[float] = (0.0, 0.0, 4.0)
     corners: np.ndarray | None = field(default=None, repr=False)
     seed: int = _capi.DEFAULT_SEED   # RT_STOCHASTIC jitter seed (flags | STOCHASTIC)
+    pfy: int | None = None           # pixelfactorY when it differs from pixelfactorX (= pf)
 
     def to_c(self) -> RtParams:
         if len(self.lights) > _capi.RT_MAX_LIGHTS:
             raise ValueError("at most 16 lights")
         p = RtParams()
-        p.width, p.height, p.pfx, p.pfy = self.width, self.height, self.pf, self.pf
+        p.width, p.height, p.pfx, p.pfy = self.width, self.height, self.pf, self.pf if self.pfy is None else self.pfy
         p.max_lvl, p.flags, p.n_lights = self.max_lvl, self.flags, len(self.lights)
         p.seed = int(self.seed)
         for i, l in enumerate(self.lights):
@@ -258,8 +259,10 @@ class Scene:
 
     def tune(self, knob: str, value: int) -> None:
         """Launch-shape knobs ('xcd_split', 'bvh_grid', 'bvh_width', 'lds_stack', 'pipes',
-        'shadow_virtual', 'pipe_batches', 'pipe_priority', 'wave_traversal', 'chain_from'); outputs
-        never depend on them."""
+        'shadow_virtual', 'pipe_batches', 'pipe_priority', 'chain_from', 'chain_split', 'top_nodes',
+        'batch_order', 'order_every', 'fuse_pixels', 'wave_steal', 'steal_half', 'steal_quarter';
+        retired, 0 only: 'wave_traversal', 'chain_refill', 'refill_grid'); outputs never depend on
+        them."""
         k = {"xcd_split": _capi.TUNE_XCD_SPLIT, "bvh_grid": _capi.TUNE_BVH_GRID,
              "bvh_width": _capi.TUNE_BVH_WIDTH, "lds_stack": _capi.TUNE_LDS_STACK,
              "pipes": _capi.TUNE_PIPES, "shadow_virtual": _capi.TUNE_SHADOW_VIRTUAL,

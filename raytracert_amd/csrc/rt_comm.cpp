@@ -145,6 +145,8 @@ int rt_assemble_tiles_device(int32_t device, int32_t width, int32_t height, int3
     if (width <= 0 || height <= 0 || tile_w <= 0 || tile_h <= 0 || frames < 1 || nranks < 1 || !d_gathered || !d_frames_out)
         return set_error(RT_E_ARG, "invalid assemble arguments");
     const int64_t T = static_cast<int64_t>((width + tile_w - 1) / tile_w) * ((height + tile_h - 1) / tile_h);
+    // tile ids g = f * T + t index the kernel's int arithmetic: the bound rt_render_tiles_device keeps
+    if (frames * T > (int64_t(1) << 30)) return set_error(RT_E_ARG, "frames x tiles exceeds 2^30");
     const int64_t slots = (frames * T + nranks - 1) / nranks;
     if (static_cast<uint64_t>(nranks) * slots * tile_w * tile_h * 3 > gathered_bytes)
         return set_error(RT_E_ARG, "gathered buffer smaller than nranks x slots tiles");

@@ -67,7 +67,6 @@ struct DevScene {
     // BVH (use_bvh != 0): nodes, leaf-ordered records and their original indices, always list
     const BvhNode *nodes;
     const TriRec *leaf_recs;
-    const float4 *leaf48;           // the leaf records as {T0, u, v, n}, 3 x float4 each (RT_LEAF48)
     const uint32_t *leaf_idx;
     const uint32_t *always;
     const TriRec *always_recs;      // the always list's records, contiguous
@@ -76,19 +75,15 @@ struct DevScene {
     int32_t bvh_depth;              // traversal stack entries needed (tree depth)
     const Bvh4Node *nodes4;         // the four-wide tree (bvh_width == 4)
     int32_t bvh_width;              // 2 or 4 (RT_TUNE_BVH_WIDTH)
-    int32_t bvh4_stack;             // four-wide stack entries needed (3 per inner level)
     int32_t lds_stack;              // stack entries per lane held in LDS (<= entries needed)
-    int32_t wave_mask;              // RT_TUNE_WAVE_TRAVERSAL: bit k closest-hit step k, bit 16+k shadow step k,
-                                    // bit 31 rt_intersect_mesh use the wave-coherent four-wide kernel
     int32_t *stack_ovf;             // deeper entries: [entry - lds_stack][grid lane], grid <= bvh_grid
     int32_t xcd_split;              // RT_TUNE_XCD_SPLIT
     int32_t bvh_grid;               // RT_TUNE_BVH_GRID
     unsigned long long *work;       // BVH kernels' work counters: [0, kWorkFields) closest-hit, then shadow
     int32_t chain_split;            // RT_TUNE_CHAIN_SPLIT: query distribution of k_chain (as xcd_split)
     int32_t top_nodes;              // RT_TUNE_TOP_NODES: four-wide nodes [0, top_nodes) read from an LDS copy
-    int32_t chain_refill;           // RT_TUNE_CHAIN_REFILL: per-lane pixel refill in the chain launch
     int32_t wave_steal;             // RT_TUNE_WAVE_STEAL: 0 off, 1 on, 2 when the chain launch is <= 2 wave rounds
-    int32_t refill_grid;            // its (resident) grid, blocks of kBvhBlock (RT_BVH_BLOCK) threads
+    int32_t resident_grid;          // chain-kernel blocks resident on the device at once (CUs x blocks per CU)
     int32_t steal_half;             // RT_TUNE_STEAL_HALF: half-wave batches of the ordered stealing launch
     int32_t steal_quarter;          // RT_TUNE_STEAL_QUARTER: quarter-wave batches before them
 };
@@ -105,10 +100,9 @@ struct DevWork {
     int32_t *counters;              // [step] main queue sizes (step 0 dense, incl. inactive), [kMaxStepsCounters + step] shadow
     int32_t *counters_next;         // in-lane fused chain launch: the next launch's counters, zeroed by this one (or null)
     int32_t *wq;                    // [2 * step + shadow] work-queue slots of kWqSlot ints (RT_TUNE_XCD_SPLIT 2)
-    int32_t *pix_out;               // per sample (fused pixel writes): its pixel's output index
-    uint32_t *batch_cost;           // chain launch: per 64-sample batch, its wave's duration (100 MHz ticks)
+    uint32_t *batch_cost;           // chain launch: per wave batch (chain_spb samples), its wave's duration (100 MHz ticks)
     int32_t *batch_order;           // chain launch: dispatch order of the batches (cost descending), or unused
-    int32_t *order_scratch;         // counting-sort scratch (kOrderKeys histogram + offsets)
+    int32_t *order_scratch;         // counting-sort scratch (kOrderBuckets histogram, then offsets)
     int64_t cap;                    // samples per batch
     int32_t steps;                  // chain steps allocated (max_lvl + 1)
 };
@@ -121,10 +115,10 @@ constexpr int kWqStride = 16;                // one 64-B line per segment counte
 constexpr int kWqSlot = 8 * kWqStride;       // eight segments (one per XCD) per launch
 
 // Launchers (all asynchronous on `stream`).
-// k_gen_primary also zeroes w.counters (then counter 0 = the batch's samples) and w.wq. fused: the
-// chain launch will write the pixels; records w.pix_out and writes the pixels outside the frame.
-void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream, bool fused = false,
-                        uint8_t *out_u8 = nullptr);
+// k_gen_primary zeroes w.counters (then counter 0 = the batch's samples) and w.wq, and writes the
+// step-0 queue of primary rays; resets_only (a fused chain launch follows, which makes its primary
+// rays itself): only the resets.
+void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream, bool resets_only = false);
 void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevWork &w, hipStream_t stream);
 void launch_closest_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream);
 void launch_shadow_gen(const DevScene &s, const DevWork &w, const ShadeParams &p, int64_t capacity, hipStream_t stream);
@@ -133,28 +127,26 @@ void launch_shadow_hit(const DevScene &s, const DevWork &w, const ShadeParams &p
 void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int64_t capacity, hipStream_t stream);
 void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream);
 // Steps first..max_lvl of every query in Q_first in one launch (closest-hit, shadows, shade per lane).
-// fuse_spp > 0 (first == 0, after launch_gen_primary(fused); fuse_spp = samples per pixel, a divisor
-// of 64): each wave writes its pixels into out_u8/out_f32 when its batch's chains end, with
-// k_frame's arithmetic, so no k_frame follows.
-// g (fused launches from step 0): the batch's frame geometry; in-lane chain kernels then make their
-// primary rays themselves (launch_gen_primary(fused) only resets the counters; primaries_inline()).
-// blocks of the chain kernels resident per CU (4 SIMDs x waves per EU x 64 / block threads)
-int chain_blocks_per_cu();
-int bvh_block_threads();   // threads per block of the BVH and chain kernels (RT_BVH_BLOCK)
-// whether launch_chain runs the per-lane refill kernel (k_chain_refill) for these arguments
-bool chain_refill_used(const DevScene &s, int fuse_spp, const FrameGeom *g);
+// fuse_spp > 0 (first == 0, g = the batch's frame geometry, fuse_spp = samples per pixel <= 64): the
+// fused frame launch. Each lane makes its sample's primary ray, folds its chain in the lane, and each
+// wave writes its pixels into out_u8/out_f32 with k_frame's arithmetic (no k_gen_primary queue, no
+// k_frame); a wave batch then holds chain_spb(fuse_spp) samples (whole pixels). Otherwise the queue
+// Q_first is traced and the chain records go to HBM for k_frame / k_fold_rays.
+// ordered: dispatch the wave batches by w.batch_order (the previous launch's measured durations).
+int chain_blocks_per_cu();   // blocks of the chain kernels resident per CU (4 SIMDs x waves per EU x 64 / block)
+int bvh_block_threads();     // threads per block of the BVH and chain kernels (RT_BVH_BLOCK)
+int chain_spb(int fuse_spp);                            // samples per wave batch of a fused launch
+int64_t chain_batches(int64_t capacity, int fuse_spp);  // wave batches of a launch over `capacity` samples
 void launch_chain(const DevScene &s, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
                   hipStream_t stream, bool ordered = false, uint8_t *out_u8 = nullptr, float *out_f32 = nullptr,
                   int fuse_spp = 0, const FrameGeom *g = nullptr);
-bool primaries_inline();
 void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t stream);
-// Batch order: the chain launch's 64-sample batches sorted by the durations it measured, longest
-// first (w.batch_cost -> w.batch_order); the next launch over the same batches dispatches in that
-// order (launch_chain(..., ordered = true)). A counting sort: one fill and three small launches.
+// Batch order: the chain launch's wave batches sorted by the durations it measured, longest first
+// (w.batch_cost -> w.batch_order); the next launch over the same batches dispatches in that order
+// (launch_chain(..., ordered = true)). A counting sort: one fill and three small launches.
 constexpr int kOrderBuckets = 128;
-constexpr int kOrderKeys = 8 * kOrderBuckets;   // (XCD segment, duration bucket) keys (RT_TUNE_BATCH_ORDER 2)
-constexpr int kWaveBatch = 64;   // samples per wave batch of the chain launch (one per lane)
-void launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream, bool xcd_segments = false);
+constexpr int kWaveBatch = 64;   // lanes per wave batch of the chain launch (one sample per lane)
+hipError_t launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream);
 void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *dst, int32_t n,
                            int32_t *idx, float4 *I, hipStream_t stream);
 // calculateNormals on the device (face normal per triangle into normals[i].xyz)

@@ -154,27 +154,10 @@ __device__ __forceinline__ void test_triangle(const TriRec &T, int t, V3 o, V3 d
     }
 }
 
-// A leaf record of the BVH: the 64-B TriRec, or (RT_LEAF48, A/B) the 48-B {T0, u, v, n} with
-// uu, uv, vv and D recomputed here in the host's order (scene_loader.cpp build_tri_records, the
-// reference's :134-136,140): the same binary32 operations, so the same bits.
-#ifndef RT_LEAF48
-#define RT_LEAF48 0
-#endif
-__device__ __forceinline__ TriRec leaf_rec(const DevScene &sc, int i) {
-    if (!RT_LEAF48) return sc.leaf_recs[i];
-    const float4 *q = sc.leaf48 + 3 * static_cast<int64_t>(i);
-    const float4 a = q[0], b = q[1], c = q[2];
-    TriRec T;
-    T.t0[0] = a.x; T.t0[1] = a.y; T.t0[2] = a.z;
-    T.u[0] = a.w; T.u[1] = b.x; T.u[2] = b.y;
-    T.v[0] = b.z; T.v[1] = b.w; T.v[2] = c.x;
-    T.n[0] = c.y; T.n[1] = c.z; T.n[2] = c.w;
-    T.uu = T.u[0] * T.u[0] + T.u[1] * T.u[1] + T.u[2] * T.u[2];
-    T.uv = T.u[0] * T.v[0] + T.u[1] * T.v[1] + T.u[2] * T.v[2];
-    T.vv = T.v[0] * T.v[0] + T.v[1] * T.v[1] + T.v[2] * T.v[2];
-    T.D = T.uv * T.uv - T.uu * T.vv;
-    return T;
-}
+// A leaf record of the BVH: the 64-B TriRec in leaf order. (A 48-B {T0, u, v, n} record with
+// uu/uv/vv/D recomputed per test cut the leaf array by a quarter and measured no faster: the walk
+// is not bound by bytes)
+__device__ __forceinline__ TriRec leaf_rec(const DevScene &sc, int i) { return sc.leaf_recs[i]; }
 
 // Scalar-load pipeline: records A and B alternate; each is fenced (s_waitcnt) before the next
 // record's s_load is issued, so one load is always in flight behind the arithmetic.
@@ -212,12 +195,9 @@ __device__ __forceinline__ void closest_hit_loop(const TriRec *__restrict__ tris
                            // 0.48 ms, C3 0.250 vs 0.259, C5 8.75 vs 8.91; C2 0.178 vs 0.171; 64: C4 0.61 ms)
 #endif
 constexpr int kBvhBlock = RT_BVH_BLOCK;
-#ifndef RT_SORT_ANYHIT
-#define RT_SORT_ANYHIT 0
-#endif
-constexpr bool kSortAnyHit = RT_SORT_ANYHIT;   // any-hit unsorted: measured 8% faster shadows
-// The BVH kernels are built for 7 waves per SIMD (<= 72 VGPRs, no spills): measured a few percent
-// faster than the unconstrained ~80 VGPRs (6 waves); 8 waves spills and is not.
+// Any-hit walks visit the wanted children unsorted (measured 8% faster shadows than sorted).
+// The per-step BVH kernels are built for 7 waves per SIMD (<= 72 VGPRs, no spills): measured a few
+// percent faster than the unconstrained ~80 VGPRs (6 waves); 8 waves spills and is not.
 
 struct RayBox { V3 o, inv; float pad, dlen; };
 
@@ -412,18 +392,6 @@ __device__ __forceinline__ float q_decode(float base, float scale, uint32_t word
     return fmaf(static_cast<float>((word >> (8 * c)) & 0xFFu), scale, base);   // q * scale is exact
 }
 
-#ifndef RT_PACKED_SLABS
-#define RT_PACKED_SLABS 0   // measured 4% slower on C4 (v_pk_fma_f32 costs two issue slots)
-#endif
-#if RT_PACKED_SLABS
-typedef float f2 __attribute__((ext_vector_type(2)));
-// q_decode for children c and c + 1 at once
-__device__ __forceinline__ f2 q_decode2(float base, float scale, uint32_t word, int c) {
-    const f2 q = f2{static_cast<float>((word >> (8 * c)) & 0xFFu), static_cast<float>((word >> (8 * c + 8)) & 0xFFu)};
-    return __builtin_elementwise_fma(q, f2{scale, scale}, f2{base, base});
-}
-#endif
-
 __device__ __forceinline__ void cswap(float &ta, int32_t &ra, float &tb, int32_t &rb) {
     const bool sw = tb < ta;
     const float t = sw ? tb : ta;
@@ -434,276 +402,52 @@ __device__ __forceinline__ void cswap(float &ta, int32_t &ra, float &tb, int32_t
     ra = r;
 }
 
-// Diagnostic build only (-DRT_STAMPS): per-lane shader-clock sums of bvh4_query's phases, read
-// through the counting instantiation of k_bvh_intersect_only (rt_work_detail, shadow fields):
-// [0] node data wait, [1] node arithmetic + stack, [2] triangle data wait, [4] triangle arithmetic,
-// [5] whole queries. The stamps serialise the loop (s_waitcnt before each), so they split a step's
-// time into its parts; they do not measure the production schedule.
-struct Stamps { unsigned long long v[6]; };
-
-// Diagnostic build only (-DRT_REGION_COUNTS): wave-level iteration counts of the chain kernel's
-// regions and the active lanes they ran with, summed per block in LDS and added to the diagnostic
-// words (rt_diag_read [0, 32)): [r] wave iterations, [16 + r] active lanes. r: 0 chain step,
-// 1 closest-hit query, 2 shadow query, 3 closest-hit node iteration, 4 closest-hit leaf iteration,
-// 5 shadow node iteration, 6 shadow leaf iteration, 7 shade. tools/region_counts.py reads them.
-#ifdef RT_REGION_COUNTS
-__shared__ unsigned long long g_rc[32];
-#define RT_RC(r) do { const uint64_t m_ = __ballot(1); \
-    if (__lane_id() == __builtin_ctzll(m_)) { atomicAdd(&g_rc[(r)], 1ull); atomicAdd(&g_rc[16 + (r)], static_cast<unsigned long long>(__popcll(m_))); } } while (0)
-#else
-#define RT_RC(r) do { } while (0)
-#endif
-#ifdef RT_STAMPS
-constexpr bool kStamps = true;
-#else
-constexpr bool kStamps = false;
-#endif
-#ifdef RT_STAMPS
-#define RT_STAMP(t) do { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); (t) = __builtin_amdgcn_s_memtime(); } while (0)
-#else
-#define RT_STAMP(t) do { (t) = 0; } while (0)
-#endif
-
-template <bool kAnyHit>
-__device__ __forceinline__ void bvh4_query(const DevScene &sc, V3 o, V3 dir, bool active, int &bidx, V3 &bI,
-                                           const LaneStack &stack, unsigned &tests, unsigned &visits,
-                                           Stamps *st = nullptr) {
-    unsigned long long q0 = 0, s0 = 0, s1 = 0, s2 = 0;
-    if (st) RT_STAMP(q0);
-    float best = FLT_MAX;
-    bool done = !active;
-    test_always<kAnyHit>(sc, o, dir, best, bidx, bI, done);
-    if (!active || (kAnyHit && done)) return;
-    // Per-ray constants. inv is clamped to |inv| <= 2^100 (dir components of 0 or below 2^-100):
-    // with the scene below 1e6 in magnitude (dev_view falls back to the binary tree otherwise)
-    // no slab distance can be NaN, and a clamped axis only narrows a slab where no hit can exist
-    // (|n.dir| >= 1e-5 needs |dir| >= 2.5e-18 there). Near and far planes are chosen once by the
-    // sign of inv, so each bound costs one byte convert and one fma.
-    V3 inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
-    constexpr float kInvMax = 0x1p100f;
-    if (!(fabsf(inv.x) <= kInvMax)) inv.x = copysignf(kInvMax, dir.x);
-    if (!(fabsf(inv.y) <= kInvMax)) inv.y = copysignf(kInvMax, dir.y);
-    if (!(fabsf(inv.z) <= kInvMax)) inv.z = copysignf(kInvMax, dir.z);
-    const float pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
-    const float dlen = sqrtf(dot(dir, dir));
-    const bool nx = inv.x < 0, ny = inv.y < 0, nz = inv.z < 0;
-    const float pnx = nx ? pad : -pad, pny = ny ? pad : -pad, pnz = nz ? pad : -pad;   // near plane = lo - pad / hi + pad
-    // distance cull: a child whose entry exceeds tcull cannot hold an accepted point nearer than
-    // best ((t dlen - pad)(1 - 1e-5) > best, with slack for this bound's own rounding)
-    float tcull = INFINITY;
-    int sp = 0;
-    int32_t ref = 0;
-    while (true) {
-        if (ref >= 0) {
-            ++visits;
-            if (st) RT_STAMP(s0);
-            uint4 a, b, c, d;
-            load_node4(stack, sc.nodes4, ref, a, b, c, d);
-            if (st) {
-                asm volatile("" ::"v"(a.x), "v"(b.x), "v"(c.x), "v"(d.x));
-                RT_STAMP(s1);
-                st->v[0] += s1 - s0;
-            }
-            const float dx = __uint_as_float(a.x) - o.x, dy = __uint_as_float(a.y) - o.y, dz = __uint_as_float(a.z) - o.z;
-            const float kx = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w)) + 127) << 23) * inv.x;
-            const float ky = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 8)) + 127) << 23) * inv.y;
-            const float kz = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 16)) + 127) << 23) * inv.z;
-            const float cnx = (dx + pnx) * inv.x, cfx = (dx - pnx) * inv.x;
-            const float cny = (dy + pny) * inv.y, cfy = (dy - pny) * inv.y;
-            const float cnz = (dz + pnz) * inv.z, cfz = (dz - pnz) * inv.z;
-            const uint32_t wnx = nx ? b.w : b.x, wfx = nx ? b.x : b.w;   // qlo / qhi words per axis
-            const uint32_t wny = ny ? c.x : b.y, wfy = ny ? b.y : c.x;
-            const uint32_t wnz = nz ? c.y : b.z, wfz = nz ? b.z : c.y;
-            int32_t rc[4] = {static_cast<int32_t>(c.z), static_cast<int32_t>(c.w), static_cast<int32_t>(d.x),
-                             static_cast<int32_t>(d.y)};
-            float tc[4];
-#if RT_PACKED_SLABS
-            // children in pairs through packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: IEEE per element,
-            // so every bound is the same value as q_decode's)
-#pragma unroll
-            for (int k = 0; k < 4; k += 2) {
-                const f2 tnx = q_decode2(cnx, kx, wnx, k), tfx = q_decode2(cfx, kx, wfx, k);
-                const f2 tny = q_decode2(cny, ky, wny, k), tfy = q_decode2(cfy, ky, wfy, k);
-                const f2 tnz = q_decode2(cnz, kz, wnz, k), tfz = q_decode2(cfz, kz, wfz, k);
-                const f2 te = f2{fmaxf(fmaxf(fmaxf(tnx.x, tny.x), tnz.x), 0.0f), fmaxf(fmaxf(fmaxf(tnx.y, tny.y), tnz.y), 0.0f)};
-                const f2 tx = f2{fminf(fminf(tfx.x, tfy.x), tfz.x), fminf(fminf(tfx.y, tfy.y), tfz.y)} * f2{1.00001f, 1.00001f};
-                bool h0 = te.x <= tx.x, h1 = te.y <= tx.y;
-                if (!kAnyHit) { h0 = h0 && te.x <= tcull; h1 = h1 && te.y <= tcull; }
-                tc[k] = h0 ? fminf(te.x, FLT_MAX) : INFINITY;
-                tc[k + 1] = h1 ? fminf(te.y, FLT_MAX) : INFINITY;
-            }
-#else
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float tnx = q_decode(cnx, kx, wnx, k), tfx = q_decode(cfx, kx, wfx, k);
-                const float tny = q_decode(cny, ky, wny, k), tfy = q_decode(cfy, ky, wfy, k);
-                const float tnz = q_decode(cnz, kz, wnz, k), tfz = q_decode(cfz, kz, wfz, k);
-                const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
-                const float tx = fminf(fminf(tfx, tfy), tfz);
-                bool h = te <= tx * 1.00001f;
-                if (!kAnyHit) h = h && te <= tcull;
-                tc[k] = h ? fminf(te, FLT_MAX) : INFINITY;   // hits sort before misses
-            }
-#endif
-            if (!kAnyHit || kSortAnyHit) {
-                // (the network costs ~25 VALU; nodes where one child or none is wanted skip it)
-                const int nh = (tc[0] != INFINITY) + (tc[1] != INFINITY) + (tc[2] != INFINITY) + (tc[3] != INFINITY);
-                if (nh > 1) {
-                cswap(tc[0], rc[0], tc[1], rc[1]);
-                cswap(tc[2], rc[2], tc[3], rc[3]);
-                cswap(tc[0], rc[0], tc[2], rc[2]);
-                cswap(tc[1], rc[1], tc[3], rc[3]);
-                cswap(tc[1], rc[1], tc[2], rc[2]);
-                } else if (nh == 1) {   // bring the one wanted child to the front
-                    const int32_t one = tc[0] != INFINITY ? rc[0] : tc[1] != INFINITY ? rc[1] : tc[2] != INFINITY ? rc[2] : rc[3];
-                    rc[0] = one;
-                    tc[0] = 0.0f;
-                    tc[1] = tc[2] = tc[3] = INFINITY;
-                }
-                if (tc[3] != INFINITY) stack.push(sp, rc[3]);
-                if (tc[2] != INFINITY) stack.push(sp, rc[2]);
-                if (tc[1] != INFINITY) stack.push(sp, rc[1]);
-                if (tc[0] != INFINITY) {
-                    ref = rc[0];
-                } else {
-                    if (sp == 0) {
-                        if (st) { RT_STAMP(s2); st->v[1] += s2 - s1; }
-                        break;
-                    }
-                    ref = stack.pop(sp);
-                }
-                if (st) { RT_STAMP(s2); st->v[1] += s2 - s1; }
-            } else {   // any-hit: any order finds the same verdict; visit the first wanted child
-                int32_t nxt = kBvhEmpty;
-                bool have = false;
-#pragma unroll
-                for (int k = 3; k >= 0; --k) {
-                    if (tc[k] != INFINITY) {
-                        if (have) stack.push(sp, nxt);
-                        nxt = rc[k];
-                        have = true;
-                    }
-                }
-                if (have) {
-                    ref = nxt;
-                } else {
-                    if (sp == 0) break;
-                    ref = stack.pop(sp);
-                }
-            }
-        } else {
-            const uint32_t u = static_cast<uint32_t>(ref);
-            const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
-            const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
-            if (st) {
-#ifdef RT_STAMPS
-                for (int k = 0; k < cnt; ++k) {
-                    RT_STAMP(s0);
-                    const TriRec T = leaf_rec(sc, first + k);
-                    asm volatile("" ::"v"(T.t0[0]), "v"(T.u[0]), "v"(T.v[0]), "v"(T.n[0]));
-                    RT_STAMP(s1);
-                    test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first + k]), o, dir, best, bidx, bI, done);
-                    RT_STAMP(s2);
-                    st->v[2] += s1 - s0;
-                    st->v[4] += s2 - s1;
-                }
-#endif
-            } else {
-                test_leaf<kAnyHit>(sc, first, cnt, o, dir, best, bidx, bI, done);
-            }
-            if (!kAnyHit && best < FLT_MAX) tcull = (best * 1.00002f + pad) / dlen * 1.00001f;
-            tests += static_cast<unsigned>(cnt);
-            if (kAnyHit && done) break;
-            if (sp == 0) break;
-            ref = stack.pop(sp);
-        }
-    }
-    if (st) { RT_STAMP(s0); st->v[5] += s0 - q0; }
-}
-
-
 // ---------------------------------------------------------------------------------------------
-// "While-while" four-wide traversal (RT_WHILE_WHILE, default; Aila & Laine 2009's speculative form):
-// a lane that reaches a leaf postpones it and keeps visiting nodes until every lane of the wave
-// holds a leaf (or has finished), then the wave tests leaves together. Node and triangle
-// arithmetic are bvh4_query's; only the interleaving of node visits and leaf tests changes, so
-// the lexicographic minimum and the any-hit verdict are the same.
+// "While-while" four-wide traversal (Aila & Laine 2009's speculative form): a lane that reaches a
+// leaf postpones it and keeps visiting nodes until every lane of the wave holds a leaf (or has
+// finished), then the wave tests leaves together, one triangle per iteration with the leaf ref as
+// the cursor. Only the interleaving of node visits and leaf tests differs from a plain walk, so the
+// lexicographic minimum and the any-hit verdict are the same. (Measured against the plain loop:
+// C4 frame 0.88 -> 0.81 ms; the cursor another 2%; any speculation slack or a second postponed
+// leaf was slower. DESIGN.md §7 records the variants that were measured and removed.)
 // ---------------------------------------------------------------------------------------------
-#ifndef RT_WHILE_WHILE
-#define RT_WHILE_WHILE 1   // measured 5% faster C4 frame, 4% C5, than bvh4_query (0; the RT_STAMPS probe uses that one)
-#endif
-#ifndef RT_WW_SLACK
-#define RT_WW_SLACK 0   // measured: 0 best (4: +5%, 12: +10%, 24: +20% frame time)
-#endif
-#ifndef RT_NODE_BRANCHFREE
-#define RT_NODE_BRANCHFREE 1
-#endif
-#ifndef RT_WW_CURSOR
-#define RT_WW_CURSOR 1   // measured 2% faster C4 and C5 than whole leaves per iteration
-#endif
-#ifndef RT_WW_LEAVES
-#define RT_WW_LEAVES 1
-#endif
 constexpr int32_t kDoneRef = kBvhEmpty;   // "no ref": a count-0 leaf is never a wanted child
 
-#ifndef RT_NF_PACKED
-#define RT_NF_PACKED 0   // 1: near/far slab planes as v_pk_fma_f32 pairs (node block 140 -> 125 VALU, yet C4
-                         // 0.481 -> 0.494 ms and C5 8.89 -> 9.30 ms: profiles/r02_ab_nf_packed.txt)
-#endif
-#ifndef RT_NODE_V2
-#define RT_NODE_V2 1   // per-ray slab offsets folded into one FMA per plane; exponent by v_ldexp_f32
-#endif
-#ifndef RT_FAST_SETUP
-#define RT_FAST_SETUP 1   // approximate reciprocals in the per-ray traversal constants (conservative margins)
-#endif
-
-// Per-ray traversal constants. With RT_NODE_V2 a child's slab plane is
+// Per-ray traversal constants. A child's slab plane is
 //   t = fma(q, 2^e * inv, fma(origin, inv, (-/+pad - o) * inv))
-// instead of fma(q, 2^e * inv, (origin - o -/+ pad) * inv): the same value up to a few ulps of
+// instead of (origin + q 2^e - o -/+ pad) * inv: the same value up to a few ulps of
 // (|o| + pad) * |inv| and of |t|, inside the pad (64 ulps of |o| + the scene's extent) and the
 // 1e-5 relative slack of the te <= tx test.
 struct Ray4 {
     V3 o, inv;
-    float pnx, pny, pnz, tcull;
-    float bnx, bny, bnz, bfx, bfy, bfz;   // RT_NODE_V2: (+/-pad - o) * inv per axis, near and far plane
-    float inv_dlen;                       // RT_FAST_SETUP: an upper bound of 1.00001 / |dir|
+    float tcull;
+    float bnx, bny, bnz, bfx, bfy, bfz;   // (+/-pad - o) * inv per axis, near and far plane
+    float inv_dlen;                       // an upper bound of 1.00001 / |dir|
     bool nx, ny, nz;
 };
 
 // tcull for the current best: no child whose entry parameter exceeds it can hold a hit at
-// distance <= best (bvh4_query). RT_FAST_SETUP multiplies by a reciprocal rounded up by 1e-4,
+// distance <= best ((t |dir| - pad)(1 - 1e-5) > best). inv_dlen is a reciprocal rounded up by 1e-4,
 // which only raises tcull (visits no fewer nodes than the division form).
-__device__ __forceinline__ float cull_param(const Ray4 &R, float best, float pad, float dlen) {
-    if (RT_FAST_SETUP) return (best * 1.00002f + pad) * R.inv_dlen;
-    return (best * 1.00002f + pad) / dlen * 1.00001f;
+__device__ __forceinline__ float cull_param(const Ray4 &R, float best, float pad) {
+    return (best * 1.00002f + pad) * R.inv_dlen;
 }
 
 // One node visit: the wanted children by entry distance, the far ones pushed; returns the next ref
-// (the nearest wanted child, else the stack top, else kDoneRef).
+// (the nearest wanted child, else the stack top, else kDoneRef). Entries [base, sp) are this walk's.
 template <bool kAnyHit>
 __device__ __forceinline__ int32_t node4_next(const Ray4 &R, uint4 a, uint4 b, uint4 c, uint4 d, const LaneStack &stack,
-                                              int &sp, int base = 0) {   // entries [base, sp) are this walk's
-    const V3 o = R.o, inv = R.inv;
-    float kx, ky, kz, cnx, cfx, cny, cfy, cnz, cfz;
-    if (RT_NODE_V2) {
-        // 2^e * inv is exact (or the same overflow) either way; v_ldexp_f32 takes the int8 exponent
-        kx = __builtin_amdgcn_ldexpf(inv.x, static_cast<int>(static_cast<int8_t>(a.w)));
-        ky = __builtin_amdgcn_ldexpf(inv.y, static_cast<int>(static_cast<int8_t>(a.w >> 8)));
-        kz = __builtin_amdgcn_ldexpf(inv.z, static_cast<int>(static_cast<int8_t>(a.w >> 16)));
-        const float ox = __uint_as_float(a.x), oy = __uint_as_float(a.y), oz = __uint_as_float(a.z);
-        cnx = fmaf(ox, inv.x, R.bnx); cfx = fmaf(ox, inv.x, R.bfx);
-        cny = fmaf(oy, inv.y, R.bny); cfy = fmaf(oy, inv.y, R.bfy);
-        cnz = fmaf(oz, inv.z, R.bnz); cfz = fmaf(oz, inv.z, R.bfz);
-    } else {
-        const float dx = __uint_as_float(a.x) - o.x, dy = __uint_as_float(a.y) - o.y, dz = __uint_as_float(a.z) - o.z;
-        kx = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w)) + 127) << 23) * inv.x;
-        ky = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 8)) + 127) << 23) * inv.y;
-        kz = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 16)) + 127) << 23) * inv.z;
-        cnx = (dx + R.pnx) * inv.x; cfx = (dx - R.pnx) * inv.x;
-        cny = (dy + R.pny) * inv.y; cfy = (dy - R.pny) * inv.y;
-        cnz = (dz + R.pnz) * inv.z; cfz = (dz - R.pnz) * inv.z;
-    }
-    const uint32_t wnx = R.nx ? b.w : b.x, wfx = R.nx ? b.x : b.w;
+                                              int &sp, int base = 0) {
+    const V3 inv = R.inv;
+    // 2^e * inv is exact (or the same overflow); v_ldexp_f32 takes the int8 exponent
+    const float kx = __builtin_amdgcn_ldexpf(inv.x, static_cast<int>(static_cast<int8_t>(a.w)));
+    const float ky = __builtin_amdgcn_ldexpf(inv.y, static_cast<int>(static_cast<int8_t>(a.w >> 8)));
+    const float kz = __builtin_amdgcn_ldexpf(inv.z, static_cast<int>(static_cast<int8_t>(a.w >> 16)));
+    const float ox = __uint_as_float(a.x), oy = __uint_as_float(a.y), oz = __uint_as_float(a.z);
+    const float cnx = fmaf(ox, inv.x, R.bnx), cfx = fmaf(ox, inv.x, R.bfx);
+    const float cny = fmaf(oy, inv.y, R.bny), cfy = fmaf(oy, inv.y, R.bfy);
+    const float cnz = fmaf(oz, inv.z, R.bnz), cfz = fmaf(oz, inv.z, R.bfz);
+    const uint32_t wnx = R.nx ? b.w : b.x, wfx = R.nx ? b.x : b.w;   // qlo / qhi words per axis
     const uint32_t wny = R.ny ? c.x : b.y, wfy = R.ny ? b.y : c.x;
     const uint32_t wnz = R.nz ? c.y : b.z, wfz = R.nz ? b.z : c.y;
     int32_t rc[4] = {static_cast<int32_t>(c.z), static_cast<int32_t>(c.w), static_cast<int32_t>(d.x),
@@ -711,24 +455,9 @@ __device__ __forceinline__ int32_t node4_next(const Ray4 &R, uint4 a, uint4 b, u
     float tc[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        float tnx, tfx, tny, tfy, tnz, tfz;
-        if (RT_NF_PACKED) {   // near and far plane of one axis in one v_pk_fma_f32 (same per-lane FMAs)
-            typedef float f2v __attribute__((ext_vector_type(2)));
-            const f2v px = __builtin_elementwise_fma(
-                f2v{static_cast<float>((wnx >> (8 * k)) & 0xFFu), static_cast<float>((wfx >> (8 * k)) & 0xFFu)},
-                f2v{kx, kx}, f2v{cnx, cfx});
-            const f2v py = __builtin_elementwise_fma(
-                f2v{static_cast<float>((wny >> (8 * k)) & 0xFFu), static_cast<float>((wfy >> (8 * k)) & 0xFFu)},
-                f2v{ky, ky}, f2v{cny, cfy});
-            const f2v pz = __builtin_elementwise_fma(
-                f2v{static_cast<float>((wnz >> (8 * k)) & 0xFFu), static_cast<float>((wfz >> (8 * k)) & 0xFFu)},
-                f2v{kz, kz}, f2v{cnz, cfz});
-            tnx = px.x; tfx = px.y; tny = py.x; tfy = py.y; tnz = pz.x; tfz = pz.y;
-        } else {
-            tnx = q_decode(cnx, kx, wnx, k); tfx = q_decode(cfx, kx, wfx, k);
-            tny = q_decode(cny, ky, wny, k); tfy = q_decode(cfy, ky, wfy, k);
-            tnz = q_decode(cnz, kz, wnz, k); tfz = q_decode(cfz, kz, wfz, k);
-        }
+        const float tnx = q_decode(cnx, kx, wnx, k), tfx = q_decode(cfx, kx, wfx, k);
+        const float tny = q_decode(cny, ky, wny, k), tfy = q_decode(cfy, ky, wfy, k);
+        const float tnz = q_decode(cnz, kz, wnz, k), tfz = q_decode(cfz, kz, wfz, k);
         const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
         const float tx = fminf(fminf(tfx, tfy), tfz);
         bool h = te <= tx * 1.00001f;
@@ -736,12 +465,12 @@ __device__ __forceinline__ int32_t node4_next(const Ray4 &R, uint4 a, uint4 b, u
         // te >= 0 (or NaN, then h is false): an integer min keeps a hit child's key below INFINITY
         tc[k] = h ? __uint_as_float(min(__float_as_uint(te), 0x7f7fffffu)) : INFINITY;
     }
-    if (RT_NODE_BRANCHFREE && (!kAnyHit || RT_NODE_BRANCHFREE > 1)) {
-        // Branch-free pushes: the wanted children after the first go to the stack with
+    if (!kAnyHit) {
+        // Sorted, branch-free pushes: the wanted children after the first go to the stack with
         // unconditional LDS writes when every lane's stack has room (slots past the new top are
         // scratch); pops the same way. Misses are INFINITY and sort last.
         const int nh = (tc[0] != INFINITY) + (tc[1] != INFINITY) + (tc[2] != INFINITY) + (tc[3] != INFINITY);
-        if (nh > 1) {
+        if (nh > 1) {   // (the 5-exchange network costs ~25 VALU; nodes with one child or none skip it)
             cswap(tc[0], rc[0], tc[1], rc[1]);
             cswap(tc[2], rc[2], tc[3], rc[3]);
             cswap(tc[0], rc[0], tc[2], rc[2]);
@@ -770,62 +499,43 @@ __device__ __forceinline__ int32_t node4_next(const Ray4 &R, uint4 a, uint4 b, u
         }
         return sp > base ? stack.pop(sp) : kDoneRef;
     }
-    if (!kAnyHit || kSortAnyHit) {
-        const int nh = (tc[0] != INFINITY) + (tc[1] != INFINITY) + (tc[2] != INFINITY) + (tc[3] != INFINITY);
-        if (nh > 1) {
-            cswap(tc[0], rc[0], tc[1], rc[1]);
-            cswap(tc[2], rc[2], tc[3], rc[3]);
-            cswap(tc[0], rc[0], tc[2], rc[2]);
-            cswap(tc[1], rc[1], tc[3], rc[3]);
-            cswap(tc[1], rc[1], tc[2], rc[2]);
-        } else if (nh == 1) {
-            const int32_t one = tc[0] != INFINITY ? rc[0] : tc[1] != INFINITY ? rc[1] : tc[2] != INFINITY ? rc[2] : rc[3];
-            rc[0] = one;
-            tc[0] = 0.0f;
-            tc[1] = tc[2] = tc[3] = INFINITY;
-        }
-        if (tc[3] != INFINITY) stack.push(sp, rc[3]);
-        if (tc[2] != INFINITY) stack.push(sp, rc[2]);
-        if (tc[1] != INFINITY) stack.push(sp, rc[1]);
-        if (tc[0] != INFINITY) return rc[0];
-    } else {
-        int32_t nxt = kDoneRef;
-        bool have = false;
+    // any-hit: any order finds the same verdict; visit the first wanted child, push the others
+    int32_t nxt = kDoneRef;
+    bool have = false;
 #pragma unroll
-        for (int k = 3; k >= 0; --k) {
-            if (tc[k] != INFINITY) {
-                if (have) stack.push(sp, nxt);
-                nxt = rc[k];
-                have = true;
-            }
+    for (int k = 3; k >= 0; --k) {
+        if (tc[k] != INFINITY) {
+            if (have) stack.push(sp, nxt);
+            nxt = rc[k];
+            have = true;
         }
-        if (have) return nxt;
     }
+    if (have) return nxt;
     return sp > base ? stack.pop(sp) : kDoneRef;
 }
 
 // The per-ray traversal constants of the four-wide walk (pad = the kernel's off-plane pad).
-// RT_FAST_SETUP: v_rcp_f32 (1 ulp) for the slab reciprocals; every plane of every node uses the
-// same inv, and a 1-ulp change of one axis' scale moves its slab parameters by 2^-23 relative,
-// inside the 1e-5 slack of the te <= tx test and the tcull bound.
-__device__ __forceinline__ void ray4_setup(const DevScene &sc, V3 o, V3 dir, Ray4 &R, float &pad, float &dlen) {
-    V3 inv = RT_FAST_SETUP ? mk(__builtin_amdgcn_rcpf(dir.x), __builtin_amdgcn_rcpf(dir.y), __builtin_amdgcn_rcpf(dir.z))
-                           : mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+// v_rcp_f32 (1 ulp) for the slab reciprocals: every plane of every node uses the same inv, and a
+// 1-ulp change of one axis' scale moves its slab parameters by 2^-23 relative, inside the 1e-5
+// slack of the te <= tx test and the tcull bound. inv is clamped to |inv| <= 2^100 (dir
+// components of 0 or below 2^-100): with the scene below 1e6 in magnitude (dev_view falls back to
+// the binary tree otherwise) no slab distance can be NaN, and a clamped axis only narrows a slab
+// where no hit can exist (|n.dir| >= 1e-5 needs |dir| >= 2.5e-18 there).
+__device__ __forceinline__ void ray4_setup(const DevScene &sc, V3 o, V3 dir, Ray4 &R, float &pad) {
+    V3 inv = mk(__builtin_amdgcn_rcpf(dir.x), __builtin_amdgcn_rcpf(dir.y), __builtin_amdgcn_rcpf(dir.z));
     constexpr float kInvMax = 0x1p100f;
     if (!(fabsf(inv.x) <= kInvMax)) inv.x = copysignf(kInvMax, dir.x);
     if (!(fabsf(inv.y) <= kInvMax)) inv.y = copysignf(kInvMax, dir.y);
     if (!(fabsf(inv.z) <= kInvMax)) inv.z = copysignf(kInvMax, dir.z);
     pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
-    const float dlen2 = dot(dir, dir);
-    dlen = RT_FAST_SETUP ? 0.0f : sqrtf(dlen2);
     // 1.00001 / |dir| with v_rsq_f32 (1 ulp) rounded up by 1e-4: never below the division form
-    R.inv_dlen = RT_FAST_SETUP ? __builtin_amdgcn_rsqf(dlen2) * 1.00011f : 0.0f;
+    R.inv_dlen = __builtin_amdgcn_rsqf(dot(dir, dir)) * 1.00011f;
     R.o = o;
     R.inv = inv;
     R.nx = inv.x < 0; R.ny = inv.y < 0; R.nz = inv.z < 0;
-    R.pnx = R.nx ? pad : -pad; R.pny = R.ny ? pad : -pad; R.pnz = R.nz ? pad : -pad;
-    R.bnx = (R.pnx - o.x) * inv.x; R.bny = (R.pny - o.y) * inv.y; R.bnz = (R.pnz - o.z) * inv.z;
-    R.bfx = (-R.pnx - o.x) * inv.x; R.bfy = (-R.pny - o.y) * inv.y; R.bfz = (-R.pnz - o.z) * inv.z;
+    const float pnx = R.nx ? pad : -pad, pny = R.ny ? pad : -pad, pnz = R.nz ? pad : -pad;   // near = lo - pad / hi + pad
+    R.bnx = (pnx - o.x) * inv.x; R.bny = (pny - o.y) * inv.y; R.bnz = (pnz - o.z) * inv.z;
+    R.bfx = (-pnx - o.x) * inv.x; R.bfy = (-pny - o.y) * inv.y; R.bfz = (-pnz - o.z) * inv.z;
     R.tcull = INFINITY;
 }
 
@@ -836,17 +546,14 @@ __device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, 
     bool done = !active;
     test_always<kAnyHit>(sc, o, dir, best, bidx, bI, done);
     if (!active || (kAnyHit && done)) return;
-    RT_RC(kAnyHit ? 2 : 1);
-    Ray4 R;   // bvh4_query's per-ray constants
-    float pad, dlen;
-    ray4_setup(sc, o, dir, R, pad, dlen);
+    Ray4 R;
+    float pad;
+    ray4_setup(sc, o, dir, R, pad);
     int sp = 0;
     int32_t node = 0;          // inner node to visit, a leaf ref, or kDoneRef
     int32_t leaf = kDoneRef;   // the postponed leaf
-    int32_t leaf2 = kDoneRef;  // a second one (RT_WW_LEAVES 2)
     while (true) {
         while (node >= 0) {
-            RT_RC(kAnyHit ? 5 : 3);
             ++visits;
             uint4 a, b, c, d;
             load_node4(stack, sc.nodes4, node, a, b, c, d);
@@ -855,42 +562,25 @@ __device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, 
                 leaf = node;
                 node = sp ? stack.pop(sp) : kDoneRef;
             }
-            if (RT_WW_LEAVES > 1 && node < 0 && node != kDoneRef && leaf2 == kDoneRef) {   // and a second one
-                leaf2 = node;
-                node = sp ? stack.pop(sp) : kDoneRef;
-            }
-            // every lane still walking holds a leaf (RT_WW_SLACK: or all but that many)
-            if (RT_WW_LEAVES > 1 ? __all(leaf2 != kDoneRef)
-                                 : RT_WW_SLACK == 0 ? __all(leaf != kDoneRef) : __popcll(__ballot(leaf == kDoneRef)) <= RT_WW_SLACK)
-                break;
+            if (__all(leaf != kDoneRef)) break;   // every lane still walking holds a leaf
         }
         while (leaf != kDoneRef) {
-            RT_RC(kAnyHit ? 6 : 4);
             const uint32_t u = static_cast<uint32_t>(leaf);
             const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
             const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
-            if (RT_WW_CURSOR) {
-                // one triangle per iteration: the ref is the cursor (first + 1, count - 1), so a lane
-                // whose leaf ends goes on to its next leaf while the others test their next triangle
-                const TriRec T = leaf_rec(sc, first);
-                test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first]), o, dir, best, bidx, bI, done);
-                ++tests;
-                if (kAnyHit && done) { node = kDoneRef; leaf2 = kDoneRef; break; }
-                if (cnt > 1) {
-                    leaf = static_cast<int32_t>(u + 1u - (1u << kBvhCountShift));
-                    continue;
-                }
-            } else {
-                test_leaf<kAnyHit>(sc, first, cnt, o, dir, best, bidx, bI, done);
-                tests += static_cast<unsigned>(cnt);
-                if (kAnyHit && done) { node = kDoneRef; leaf2 = kDoneRef; break; }
+            // one triangle per iteration: the ref is the cursor (first + 1, count - 1), so a lane
+            // whose leaf ends goes on to its next leaf while the others test their next triangle
+            const TriRec T = leaf_rec(sc, first);
+            test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first]), o, dir, best, bidx, bI, done);
+            ++tests;
+            if (kAnyHit && done) { node = kDoneRef; break; }
+            if (cnt > 1) {
+                leaf = static_cast<int32_t>(u + 1u - (1u << kBvhCountShift));
+                continue;
             }
-            if (!kAnyHit && best < FLT_MAX) R.tcull = cull_param(R, best, pad, dlen);
+            if (!kAnyHit && best < FLT_MAX) R.tcull = cull_param(R, best, pad);
             leaf = kDoneRef;
-            if (RT_WW_LEAVES > 1 && leaf2 != kDoneRef) {
-                leaf = leaf2;
-                leaf2 = kDoneRef;
-            } else if (node < 0 && node != kDoneRef) {
+            if (node < 0 && node != kDoneRef) {
                 leaf = node;
                 node = sp ? stack.pop(sp) : kDoneRef;
             }
@@ -898,7 +588,6 @@ __device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, 
         if (node == kDoneRef) break;
     }
 }
-
 // ---------------------------------------------------------------------------------------------
 // While-while walk with in-wave work stealing (RT_TUNE_WAVE_STEAL, chain launch): a lane whose own query is finished
 // takes the bottom entry of another lane's traversal stack (a subtree that lane would visit later)
@@ -942,8 +631,8 @@ __device__ __forceinline__ void bvh4_query_steal(const DevScene &sc, V3 o, V3 di
     s_key[tid] = kNoKey;
     // o, dir: the ray this lane walks (its own, later the rays it helps with)
     Ray4 R;
-    float pad, dlen;
-    ray4_setup(sc, o, dir, R, pad, dlen);
+    float pad;
+    ray4_setup(sc, o, dir, R, pad);
     int sp = 0, base = 0;
     int32_t node = (active && !(kAnyHit && done)) ? 0 : kDoneRef;
     int32_t leaf = kDoneRef;
@@ -968,7 +657,7 @@ __device__ __forceinline__ void bvh4_query_steal(const DevScene &sc, V3 o, V3 di
                 best = __uint_as_float(static_cast<uint32_t>(sk >> 32));
                 bidx = static_cast<int>(static_cast<uint32_t>(sk));
                 pidx = bidx;
-                if (!kAnyHit) R.tcull = cull_param(R, best, pad, dlen);
+                if (!kAnyHit) R.tcull = cull_param(R, best, pad);
             }
         }
         if (node == kDoneRef && leaf == kDoneRef) { owner = -1; sp = base; }   // (an abandoned any-hit walk's stack too)
@@ -1007,8 +696,8 @@ __device__ __forceinline__ void bvh4_query_steal(const DevScene &sc, V3 o, V3 di
             if (helper) {
                 o = ho; dir = hd;
                 best = hb; bidx = hi; pidx = hi;   // the donor's best bounds the final minimum: cull with it
-                ray4_setup(sc, o, dir, R, pad, dlen);
-                if (!kAnyHit && best < FLT_MAX) R.tcull = cull_param(R, best, pad, dlen);
+                ray4_setup(sc, o, dir, R, pad);
+                if (!kAnyHit && best < FLT_MAX) R.tcull = cull_param(R, best, pad);
                 done = false;
                 sp = 0; base = 0;
                 node = ref;
@@ -1039,7 +728,7 @@ __device__ __forceinline__ void bvh4_query_steal(const DevScene &sc, V3 o, V3 di
                 leaf = static_cast<int32_t>(u + 1u - (1u << kBvhCountShift));
                 continue;
             }
-            if (!kAnyHit && best < FLT_MAX) R.tcull = cull_param(R, best, pad, dlen);
+            if (!kAnyHit && best < FLT_MAX) R.tcull = cull_param(R, best, pad);
             leaf = kDoneRef;
             if (node < 0 && node != kDoneRef) {
                 leaf = node;
@@ -1057,256 +746,14 @@ __device__ __forceinline__ void bvh4_query_steal(const DevScene &sc, V3 o, V3 di
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Two shadow queries of one hit in one walk (isShadow for lights l and l+1, raytracing.cpp:241-261):
-// both rays start at the same point, so they share the node frame offset and the pad; each keeps
-// its own slab arithmetic (bvh4_query's, per ray), its own cull distance and verdict. A child is
-// visited when either ray wants it, so each ray reaches every leaf its own walk would (and tests
-// a superset of its triangles, which cannot change a lexicographic minimum or an any-hit
-// verdict); a ray that is finished (any-hit accepted) wants nothing. The node and triangle
-// records are fetched once for both rays: half the dependent loads of two separate walks.
-// ---------------------------------------------------------------------------------------------
-#ifndef RT_SHADOW_PAIRS
-#define RT_SHADOW_PAIRS 0   // measured slower on C4 (1.04 vs 0.88 ms) and C5: the second ray's slab and
-                            // triangle arithmetic costs more than the shared fetches save
-#endif
-struct PairRay {
-    V3 dir, inv;
-    float dlen, tcull, best;
-    int bidx;
-    bool done;
-};
 
-__device__ __forceinline__ void pair_ray_init(PairRay &r, V3 dir) {
-    r.dir = dir;
-    V3 inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
-    constexpr float kInvMax = 0x1p100f;   // see bvh4_query
-    if (!(fabsf(inv.x) <= kInvMax)) inv.x = copysignf(kInvMax, dir.x);
-    if (!(fabsf(inv.y) <= kInvMax)) inv.y = copysignf(kInvMax, dir.y);
-    if (!(fabsf(inv.z) <= kInvMax)) inv.z = copysignf(kInvMax, dir.z);
-    r.inv = inv;
-    r.dlen = sqrtf(dot(dir, dir));
-    r.tcull = INFINITY;
-}
-
-// Entry distances of the four children for one ray (INFINITY: not wanted), bvh4_query's arithmetic.
-template <bool kAnyHit>
-__device__ __forceinline__ void pair_children(const PairRay &r, float pad, float dx, float dy, float dz, uint4 a, uint4 b,
-                                              uint4 c, float (&tc)[4]) {
-    const V3 inv = r.inv;
-    const bool nx = inv.x < 0, ny = inv.y < 0, nz = inv.z < 0;
-    const float pnx = nx ? pad : -pad, pny = ny ? pad : -pad, pnz = nz ? pad : -pad;
-    const float kx = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w)) + 127) << 23) * inv.x;
-    const float ky = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 8)) + 127) << 23) * inv.y;
-    const float kz = __int_as_float((static_cast<int>(static_cast<int8_t>(a.w >> 16)) + 127) << 23) * inv.z;
-    const float cnx = (dx + pnx) * inv.x, cfx = (dx - pnx) * inv.x;
-    const float cny = (dy + pny) * inv.y, cfy = (dy - pny) * inv.y;
-    const float cnz = (dz + pnz) * inv.z, cfz = (dz - pnz) * inv.z;
-    const uint32_t wnx = nx ? b.w : b.x, wfx = nx ? b.x : b.w;
-    const uint32_t wny = ny ? c.x : b.y, wfy = ny ? b.y : c.x;
-    const uint32_t wnz = nz ? c.y : b.z, wfz = nz ? b.z : c.y;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const float tnx = q_decode(cnx, kx, wnx, k), tfx = q_decode(cfx, kx, wfx, k);
-        const float tny = q_decode(cny, ky, wny, k), tfy = q_decode(cfy, ky, wfy, k);
-        const float tnz = q_decode(cnz, kz, wnz, k), tfz = q_decode(cfz, kz, wfz, k);
-        const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
-        const float tx = fminf(fminf(tfx, tfy), tfz);
-        bool h = te <= tx * 1.00001f && !r.done;
-        if (!kAnyHit) h = h && te <= r.tcull;
-        tc[k] = h ? fminf(te, FLT_MAX) : INFINITY;
-    }
-}
-
-template <bool kAnyHit>
-__device__ __forceinline__ void bvh4_query_pair(const DevScene &sc, V3 o, PairRay &r0, PairRay &r1,
-                                                const LaneStack &stack, unsigned &tests, unsigned &visits) {
-    V3 dummy = mk(0, 0, 0);
-    test_always<kAnyHit>(sc, o, r0.dir, r0.best, r0.bidx, dummy, r0.done);
-    test_always<kAnyHit>(sc, o, r1.dir, r1.best, r1.bidx, dummy, r1.done);
-    if (kAnyHit && r0.done && r1.done) return;
-    const float pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
-    int sp = 0;
-    int32_t ref = 0;
-    while (true) {
-        if (ref >= 0) {
-            ++visits;
-            uint4 a, b, c, d;
-            load_node4(stack, sc.nodes4, ref, a, b, c, d);
-            const float dx = __uint_as_float(a.x) - o.x, dy = __uint_as_float(a.y) - o.y, dz = __uint_as_float(a.z) - o.z;
-            float t0[4], t1[4];
-            pair_children<kAnyHit>(r0, pad, dx, dy, dz, a, b, c, t0);
-            pair_children<kAnyHit>(r1, pad, dx, dy, dz, a, b, c, t1);
-            int32_t rc[4] = {static_cast<int32_t>(c.z), static_cast<int32_t>(c.w), static_cast<int32_t>(d.x),
-                             static_cast<int32_t>(d.y)};
-            float tc[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) tc[k] = fminf(t0[k], t1[k]);   // wanted by either ray
-            const int nh = (tc[0] != INFINITY) + (tc[1] != INFINITY) + (tc[2] != INFINITY) + (tc[3] != INFINITY);
-            if (nh > 1) {
-                cswap(tc[0], rc[0], tc[1], rc[1]);
-                cswap(tc[2], rc[2], tc[3], rc[3]);
-                cswap(tc[0], rc[0], tc[2], rc[2]);
-                cswap(tc[1], rc[1], tc[3], rc[3]);
-                cswap(tc[1], rc[1], tc[2], rc[2]);
-            } else if (nh == 1) {
-                const int32_t one = tc[0] != INFINITY ? rc[0] : tc[1] != INFINITY ? rc[1] : tc[2] != INFINITY ? rc[2] : rc[3];
-                rc[0] = one;
-                tc[0] = 0.0f;
-                tc[1] = tc[2] = tc[3] = INFINITY;
-            }
-            if (tc[3] != INFINITY) stack.push(sp, rc[3]);
-            if (tc[2] != INFINITY) stack.push(sp, rc[2]);
-            if (tc[1] != INFINITY) stack.push(sp, rc[1]);
-            if (tc[0] != INFINITY) {
-                ref = rc[0];
-            } else {
-                if (sp == 0) break;
-                ref = stack.pop(sp);
-            }
-        } else {
-            const uint32_t u = static_cast<uint32_t>(ref);
-            const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
-            const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
-            for (int k = 0; k < cnt; ++k) {
-                const TriRec T = leaf_rec(sc, first + k);
-                const int t = static_cast<int>(sc.leaf_idx[first + k]);
-                test_triangle<kAnyHit, true>(T, t, o, r0.dir, r0.best, r0.bidx, dummy, r0.done);
-                test_triangle<kAnyHit, true>(T, t, o, r1.dir, r1.best, r1.bidx, dummy, r1.done);
-            }
-            if (!kAnyHit) {
-                if (r0.best < FLT_MAX) r0.tcull = (r0.best * 1.00002f + pad) / r0.dlen * 1.00001f;
-                if (r1.best < FLT_MAX) r1.tcull = (r1.best * 1.00002f + pad) / r1.dlen * 1.00001f;
-            }
-            tests += static_cast<unsigned>(cnt);
-            if (kAnyHit && r0.done && r1.done) break;
-            if (sp == 0) break;
-            ref = stack.pop(sp);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Wave-coherent four-wide traversal (W = 5): the 64 lanes of a wave walk ONE path through the
-// tree. A node's child is visited when any lane's box test (same arithmetic as bvh4_query) wants
-// it, so every lane still visits every node its own traversal would and tests a superset of its
-// triangles; the lexicographic minimum is order-independent, so results are identical. What it
-// buys for coherent rays (a tile's primaries, their shadow rays): node and triangle records are
-// wave-uniform, fetched by scalar loads into SGPRs instead of 64 vector loads of the same bytes,
-// the stack is one wave-uniform LDS column, and there is no per-lane divergence in the loop.
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ int32_t uniform(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-
-template <bool kAnyHit>
-__device__ __forceinline__ void wave_query(const DevScene &sc, const Bvh4Node *__restrict__ nodes,
-                                           const TriRec *__restrict__ recs, const uint32_t *__restrict__ ridx, V3 o,
-                                           V3 dir, bool active, int &bidx, V3 &bI, int32_t *wstack, unsigned &tests,
-                                           unsigned &visits) {
-    float best = FLT_MAX;
-    bool done = !active;
-    test_always<kAnyHit>(sc, o, dir, best, bidx, bI, done);
-    if (!__any(!done)) return;
-    V3 inv = mk(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
-    constexpr float kInvMax = 0x1p100f;   // see bvh4_query
-    if (!(fabsf(inv.x) <= kInvMax)) inv.x = copysignf(kInvMax, dir.x);
-    if (!(fabsf(inv.y) <= kInvMax)) inv.y = copysignf(kInvMax, dir.y);
-    if (!(fabsf(inv.z) <= kInvMax)) inv.z = copysignf(kInvMax, dir.z);
-    const float pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
-    const float dlen = sqrtf(dot(dir, dir));
-    const bool nx = inv.x < 0, ny = inv.y < 0, nz = inv.z < 0;
-    const float pnx = nx ? pad : -pad, pny = ny ? pad : -pad, pnz = nz ? pad : -pad;
-    float tcull = done ? -INFINITY : INFINITY;   // a finished lane wants no child
-    int sp = 0;
-    int32_t ref = 0;
-    while (true) {
-        if (ref >= 0) {
-            ++visits;
-            const Bvh4Node &nd = nodes[ref];
-            const uint32_t aw = static_cast<uint32_t>(static_cast<uint8_t>(nd.ex[0])) |
-                                (static_cast<uint32_t>(static_cast<uint8_t>(nd.ex[1])) << 8) |
-                                (static_cast<uint32_t>(static_cast<uint8_t>(nd.ex[2])) << 16);
-            const float dx = nd.origin[0] - o.x, dy = nd.origin[1] - o.y, dz = nd.origin[2] - o.z;
-            const float kx = __int_as_float((static_cast<int>(static_cast<int8_t>(aw)) + 127) << 23) * inv.x;
-            const float ky = __int_as_float((static_cast<int>(static_cast<int8_t>(aw >> 8)) + 127) << 23) * inv.y;
-            const float kz = __int_as_float((static_cast<int>(static_cast<int8_t>(aw >> 16)) + 127) << 23) * inv.z;
-            const float cnx = (dx + pnx) * inv.x, cfx = (dx - pnx) * inv.x;
-            const float cny = (dy + pny) * inv.y, cfy = (dy - pny) * inv.y;
-            const float cnz = (dz + pnz) * inv.z, cfz = (dz - pnz) * inv.z;
-            const uint32_t wnx = nx ? nd.qhi[0] : nd.qlo[0], wfx = nx ? nd.qlo[0] : nd.qhi[0];
-            const uint32_t wny = ny ? nd.qhi[1] : nd.qlo[1], wfy = ny ? nd.qlo[1] : nd.qhi[1];
-            const uint32_t wnz = nz ? nd.qhi[2] : nd.qlo[2], wfz = nz ? nd.qlo[2] : nd.qhi[2];
-            float key[4];
-            int32_t rc[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float tnx = q_decode(cnx, kx, wnx, k), tfx = q_decode(cfx, kx, wfx, k);
-                const float tny = q_decode(cny, ky, wny, k), tfy = q_decode(cfy, ky, wfy, k);
-                const float tnz = q_decode(cnz, kz, wnz, k), tfz = q_decode(cfz, kz, wfz, k);
-                const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
-                const float tx = fminf(fminf(tfx, tfy), tfz);
-                const bool h = te <= tx * 1.00001f && te <= tcull;
-                const unsigned long long m = __ballot(h);
-                rc[k] = nd.child[k];
-                // the wave's order key: the entry distance of the first lane that wants the child
-                key[k] = (m && rc[k] != kBvhEmpty)
-                             ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fminf(te, FLT_MAX)),
-                                                                        __ffsll(static_cast<long long>(m)) - 1))
-                             : INFINITY;
-            }
-            cswap(key[0], rc[0], key[1], rc[1]);
-            cswap(key[2], rc[2], key[3], rc[3]);
-            cswap(key[0], rc[0], key[2], rc[2]);
-            cswap(key[1], rc[1], key[3], rc[3]);
-            cswap(key[1], rc[1], key[2], rc[2]);
-            if (key[3] != INFINITY) { if (__lane_id() == 0) wstack[sp] = rc[3]; ++sp; }
-            if (key[2] != INFINITY) { if (__lane_id() == 0) wstack[sp] = rc[2]; ++sp; }
-            if (key[1] != INFINITY) { if (__lane_id() == 0) wstack[sp] = rc[1]; ++sp; }
-            if (key[0] != INFINITY) {
-                ref = uniform(rc[0]);
-            } else {
-                if (sp == 0) break;
-                ref = uniform(wstack[--sp]);
-            }
-        } else {
-            const uint32_t u = static_cast<uint32_t>(ref);
-            const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
-            const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
-            for (int k = 0; k < cnt; ++k) {
-                const TriRec T = recs[first + k];
-                if (!done) test_triangle<kAnyHit, true>(T, static_cast<int>(ridx[first + k]), o, dir, best, bidx, bI, done);
-            }
-            tests += static_cast<unsigned>(cnt);
-            if (kAnyHit) {
-                if (done) tcull = -INFINITY;
-                if (!__any(!done)) break;
-            } else if (best < FLT_MAX) {
-                tcull = (best * 1.00002f + pad) / dlen * 1.00001f;
-            }
-            if (sp == 0) break;
-            ref = uniform(wstack[--sp]);
-        }
-    }
-}
-
-// Scalar-loadable views of the four-wide tree (kernel arguments marked __restrict__, so the
-// compiler may fetch wave-uniform records with s_load).
-struct TreeArgs {
-    const Bvh4Node *nodes;
-    const TriRec *recs;
-    const uint32_t *idx;
-};
-
+// The closest-hit / any-hit query of the tree kernels: W = 4 the four-wide while-while walk (or,
+// kSteal, its in-wave stealing form), W = 2 the binary tree (scenes above 1e6 in magnitude).
 template <bool kAnyHit, int W, bool kSteal = false>
-__device__ __forceinline__ void bvh_query_w(const DevScene &sc, const Bvh4Node *__restrict__ n4,
-                                            const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx,
-                                            int32_t *lds, V3 o, V3 dir, bool active, int &bidx, V3 &bI,
-                                            const LaneStack &stack, unsigned &tests, unsigned &visits,
-                                            Stamps *st = nullptr) {
-    if (W == 5) wave_query<kAnyHit>(sc, n4, lrec, lidx, o, dir, active, bidx, bI, lds + (threadIdx.x >> 6) * sc.bvh4_stack,
-                                    tests, visits);
-    else if (W == 4 && kSteal && !st) bvh4_query_steal<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
-    else if (W == 4 && RT_WHILE_WHILE && !st) bvh4_query_ww<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
-    else if (W == 4) bvh4_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits, st);
+__device__ __forceinline__ void bvh_query_w(const DevScene &sc, V3 o, V3 dir, bool active, int &bidx, V3 &bI,
+                                            const LaneStack &stack, unsigned &tests, unsigned &visits) {
+    if (W == 4 && kSteal) bvh4_query_steal<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
+    else if (W == 4) bvh4_query_ww<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
     else bvh_query<kAnyHit>(sc, o, dir, active, bidx, bI, stack, tests, visits);
 }
 
@@ -1434,9 +881,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(7))) 
                                                                const float4 *__restrict__ q_dst,
                                                                const int32_t *__restrict__ q_count,
                                                                int32_t *__restrict__ hit_idx, float4 *__restrict__ hit_I,
-                                                               int32_t *__restrict__ wq, const Bvh4Node *__restrict__ n4,
-                                                               const TriRec *__restrict__ lrec,
-                                                               const uint32_t *__restrict__ lidx) {
+                                                               int32_t *__restrict__ wq) {
     extern __shared__ int32_t lds_stack[];
     const LaneStack stack = lane_stack(sc, lds_stack);
     WorkTally<kCount> wt;
@@ -1452,7 +897,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(7))) 
         int bidx = -1;
         V3 bI = mk(0, 0, 0);
         wt.begin();
-        bvh_query_w<false, W>(sc, n4, lrec, lidx, lds_stack, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
+        bvh_query_w<false, W>(sc, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
         wt.end();
         if (j < end) {
             hit_idx[j] = bidx;
@@ -1501,9 +946,7 @@ __device__ __forceinline__ void add_pair_count(const ShadowSource &src, unsigned
 
 template <bool kAnyHit, int W, bool kCount>
 __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(7))) void k_bvh_shadow_hit(const DevScene sc, const ShadowSource src,
-                                                              uint8_t *__restrict__ shadow, int32_t *__restrict__ wq,
-                                                              const Bvh4Node *__restrict__ n4, const TriRec *__restrict__ lrec,
-                                                              const uint32_t *__restrict__ lidx) {
+                                                              uint8_t *__restrict__ shadow, int32_t *__restrict__ wq) {
     extern __shared__ int32_t lds_stack[];
     const LaneStack stack = lane_stack(sc, lds_stack);
     WorkTally<kCount> wt;
@@ -1516,7 +959,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(7))) 
         int bidx = -1;
         V3 bI = mk(0, 0, 0);
         wt.begin();
-        bvh_query_w<kAnyHit, W>(sc, n4, lrec, lidx, lds_stack, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
+        bvh_query_w<kAnyHit, W>(sc, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
         wt.end();
         if (active) {
             uint8_t sh = 0;
@@ -1531,14 +974,10 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(7))) 
 template <int W, bool kCount>
 __global__ __launch_bounds__(kBvhBlock) void k_bvh_intersect_only(const DevScene sc, const float4 *__restrict__ q_org,
                                                                   const float4 *__restrict__ q_dst, int n,
-                                                                  int32_t *__restrict__ idx, float4 *__restrict__ I,
-                                                                  const Bvh4Node *__restrict__ n4,
-                                                                  const TriRec *__restrict__ lrec,
-                                                                  const uint32_t *__restrict__ lidx) {
+                                                                  int32_t *__restrict__ idx, float4 *__restrict__ I) {
     extern __shared__ int32_t lds_stack[];
     const LaneStack stack = lane_stack(sc, lds_stack);
     WorkTally<kCount> wt;
-    Stamps stamps = {};
     drive_queries(n, 0, nullptr, [&](int j, int end) {
         const bool active = j < end;
         V3 o = mk(0, 0, 0), dir = mk(0, 0, 0);
@@ -1550,19 +989,11 @@ __global__ __launch_bounds__(kBvhBlock) void k_bvh_intersect_only(const DevScene
         int bidx = -1;
         V3 bI = mk(0, 0, 0);
         wt.begin();
-        bvh_query_w<false, W>(sc, n4, lrec, lidx, lds_stack, o, dir, active, bidx, bI, stack, wt.tests, wt.visits,
-                              kStamps && kCount ? &stamps : nullptr);
+        bvh_query_w<false, W>(sc, o, dir, active, bidx, bI, stack, wt.tests, wt.visits);
         wt.end();
         if (active) { idx[j] = bidx; I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f); }
     });
     wt.flush(sc.work);
-    if (kStamps && kCount && sc.work) {   // (diagnostic build) per-wave sums into the shadow fields
-        for (int f = 0; f < 6; ++f) {
-            unsigned long long v = stamps.v[f];
-            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-            if (__lane_id() == 0 && f != 3) atomicAdd(&sc.work[kWorkFields + f], v);
-        }
-    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_closest_hit(const TriRec *__restrict__ tris, int nt,
@@ -1706,26 +1137,19 @@ __device__ __forceinline__ bool primary_sample(const FrameGeom &g, int64_t s, V3
 }
 
 // Also resets the batch's queue counters and work-queue slots (counter 0 = the queue's size), so
-// no separate fills precede the batch. fused 1 (the chain launch writes the pixels): also records
-// each sample's pixel index in w.pix_out and writes the pixels outside the frame black in the
-// tile-major layout, as k_frame does. fused 2 (RT_PRIMARY_INLINE): the resets only; the chain
-// launch makes each primary ray in its lane (primary_sample) and writes those pixels itself.
-__global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWork w, uint8_t *__restrict__ fused_u8,
-                                                        int fused) {
+// no separate fills precede the batch. resets_only (the fused chain launch follows, which makes
+// each primary ray in its lane with primary_sample and writes the pixels itself): nothing else.
+__global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWork w, int resets_only) {
     const int spp = g.pfx * g.pfy;
     const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th * spp;
     const int64_t s = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (s < 2 * kMaxStepsCounters) w.counters[s] = s == 0 ? static_cast<int32_t>(n) : 0;
     if (s < 2 * static_cast<int64_t>(w.steps) * kWqSlot) w.wq[s] = 0;
-    if (s >= n || fused == 2) return;   // 2: the chain launch generates its primaries itself
+    if (s >= n || resets_only) return;
     V3 origin, dest;
     int64_t px;
     int sub;
     const bool valid = primary_sample(g, s, origin, dest, px, sub);
-    if (fused) {
-        if (valid) w.pix_out[s] = static_cast<int32_t>(px);
-        else if (g.out_mode == 0 && fused_u8 && sub == 0) { fused_u8[3 * px] = 0; fused_u8[3 * px + 1] = 0; fused_u8[3 * px + 2] = 0; }
-    }
     w.depth[s] = 0;
     w.q_org[0][s] = make_float4(origin.x, origin.y, origin.z, as_float(static_cast<int>(s)));
     w.q_dst[0][s] = make_float4(dest.x, dest.y, dest.z, as_float(valid ? 0 : -1));
@@ -1782,18 +1206,12 @@ struct Secondary {
     uint32_t code;      // in-lane chain records: state | coefficient kind << 2 | material << 3
 };
 
-// In-lane chain (RT_CHAIN_INLANE, the fused chain launch): a step's record is written only when
-// the step has a child, as 16 B {local colour, code}, where the code names the child's coefficient
-// by the hit material (kind 0: Ks, reflection and the acos branch of refraction; kind 1: (1 - Tr)
-// broadcast, transmission: raytracing.cpp:298-328,361-363), so the fold re-derives the same floats;
-// the chain's last step stays in registers and the lane folds its chain itself.
-#ifndef RT_PRIMARY_INLINE
-#define RT_PRIMARY_INLINE 1   // in-lane chain launches make their primary rays themselves (no primary queue)
-#endif
-#ifndef RT_CHAIN_INLANE
-#define RT_CHAIN_INLANE 1   // measured neutral in time (C4 0.499 vs 0.500-0.51 ms, C5 grid 0.65 both) with
-                            // fewer bytes written and read back; bit-identical frames
-#endif
+// In-lane chain (the fused chain launch): a step's record is written only when the step has a
+// child, as 16 B {local colour, code}, where the code names the child's coefficient by the hit
+// material (kind 0: Ks, reflection and the acos branch of refraction; kind 1: (1 - Tr) broadcast,
+// transmission: raytracing.cpp:298-328,361-363), so the fold re-derives the same floats; the
+// chain's last step stays in registers and the lane folds its chain itself. (Against 32-B records
+// of every step: bytes written past L2 265 -> 104 MB per C4 launch, time unchanged.)
 constexpr uint32_t kCoefTr = 4u;
 
 // A chain record store. RT_CHAIN_SC1 (A/B build): written through past L2 (sc1), so the records,
@@ -2054,17 +1472,14 @@ constexpr int kChainSteps = 256;   // max_lvl <= 254
 // of the chain. Shadow-ray statistics are counted per block in s_sh.
 template <bool kAnyHit, int W, bool kCount, bool kInLane = false, bool kSteal = false>
 __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeParams &p, const DevWork &w, int step,
-                                                int sample, V3 org, V3 dst, int lvl, const LaneStack &stack,
-                                                int32_t *lds_stack, const Bvh4Node *__restrict__ n4,
-                                                const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx,
-                                                int *s_sh, WorkTally<kCount> &wc, WorkTally<kCount> &ws) {
-    RT_RC(0);
+                                                int sample, V3 org, V3 dst, int lvl, const LaneStack &stack, int *s_sh,
+                                                WorkTally<kCount> &wc, WorkTally<kCount> &ws) {
     Secondary none;
     none.state = kChildNone;
     none.local = mk(0, 0, 0);   // trace() miss: black (:389-391)
     int bidx = -1;
     V3 bI = mk(0, 0, 0);
-    bvh_query_w<false, W, kSteal>(sc, n4, lrec, lidx, lds_stack, org, sub(dst, org), true, bidx, bI, stack, wc.tests, wc.visits);
+    bvh_query_w<false, W, kSteal>(sc, org, sub(dst, org), true, bidx, bI, stack, wc.tests, wc.visits);
     if (bidx >= sc.nt) { w.counters[kErrorSlot] = 1; bidx = -1; }
     if (bidx < 0) {
         if (!kInLane) shade_miss(w, step, sample);
@@ -2075,101 +1490,92 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
     if (shadows) {
         atomicAdd(&s_sh[step], p.n_lights);
         const V3 so = mk(bI.x + 0.1f, bI.y + 0.1f, bI.z + 0.1f);                // :248
-        int l = 0;
-        if (W == 4 && RT_SHADOW_PAIRS) {   // two lights per walk (bvh4_query_pair)
-            for (; l + 1 < p.n_lights; l += 2) {
-                PairRay r0, r1;
-                r0.best = r1.best = FLT_MAX;
-                r0.bidx = r1.bidx = -1;
-                r0.done = r1.done = false;
-                pair_ray_init(r0, mk(p.lights[l][0] - so.x, p.lights[l][1] - so.y, p.lights[l][2] - so.z));
-                pair_ray_init(r1, mk(p.lights[l + 1][0] - so.x, p.lights[l + 1][1] - so.y, p.lights[l + 1][2] - so.z));
-                bvh4_query_pair<kAnyHit>(sc, so, r0, r1, stack, ws.tests, ws.visits);
-                if (r0.bidx >= 0 && !sc.mats[sc.tri_mat[r0.bidx]].transparent) mask |= 1u << l;         // :253-257
-                if (r1.bidx >= 0 && !sc.mats[sc.tri_mat[r1.bidx]].transparent) mask |= 1u << (l + 1);
-            }
-        }
-        for (; l < p.n_lights; ++l) {
+        for (int l = 0; l < p.n_lights; ++l) {
             int sidx = -1;
             V3 sI = mk(0, 0, 0);
             const V3 sd = mk(p.lights[l][0] - so.x, p.lights[l][1] - so.y, p.lights[l][2] - so.z);
-            bvh_query_w<kAnyHit, W, kSteal>(sc, n4, lrec, lidx, lds_stack, so, sd, true, sidx, sI, stack, ws.tests, ws.visits);
+            bvh_query_w<kAnyHit, W, kSteal>(sc, so, sd, true, sidx, sI, stack, ws.tests, ws.visits);
             if (sidx >= 0 && !sc.mats[sc.tri_mat[sidx]].transparent) mask |= 1u << l;   // :253-257
         }
     }
-    RT_RC(7);
     return shade_hit<kInLane>(sc, p, w, step, sample, sub(dst, org), lvl, bidx, bI, [&](int l) { return ((mask >> l) & 1u) != 0; });
 }
 
-// Chain tail (RT_TUNE_CHAIN_FROM): the remaining steps of every query in Q_first, each lane
-// carrying its own ray through closest-hit, its shadow rays and shade until its chain ends. With
-// no launch boundary between steps, a lane's next step does not wait for the slowest wave of the
-// current one, which is what the thin last steps spend their time on. The per-ray arithmetic is
-// the per-step kernels' own (the same functions). Query counts per step (ray statistics) are
-// summed per block in LDS and added to the step counters once at the end.
-// Batch order (ordered): wave-sized batch v of the grid-stride walk takes the samples of batch
-// w.batch_order[v]; every wave records its batch's duration in w.batch_cost, from which
-// launch_order_batches prepares the next launch's order (longest first, so the deep reflection
-// chains of a frame start at once instead of trailing it). Placement never changes results.
+// The chain launch: steps first..max_lvl of every query, each lane carrying its own ray through
+// closest-hit, its shadow rays and shade until its chain ends. With no launch boundary between
+// steps, a lane's next step does not wait for the slowest wave of the current one, which is what
+// the thin last steps of a per-step wavefront spend their time on. The per-ray arithmetic is the
+// per-step kernels' own (the same functions). Query counts per step (ray statistics) are summed per
+// block in LDS and added to the step counters once at the end.
+//
+// Batches. The launch walks wave-sized batches: batch b is lanes 0..63 of one wave. kInLane (the
+// fused frame launch, from step 0): batch b holds samples [b * spb, b * spb + spb) with spb =
+// floor(64 / spp) * spp, so a pixel's spp sub-samples sit in adjacent lanes of one wave (pf 3: 7
+// pixels x 9 sub-samples in 63 lanes); each lane makes its primary ray (main.cpp:377-386), folds its
+// chain back to front in the lane (c_k = local_k + coef_k * c_{k+1}, the order in which trace()
+// results are added, raytracing.cpp:359,363), and the wave sums a pixel's sub-samples with lane
+// shuffles in k_frame's order and writes the pixel. Otherwise (a tail from step first > 0, or
+// rt_trace_rays) batch b is queries [64 b, 64 b + 64) of the step's queue and the chain records
+// go to HBM for k_frame / k_fold_rays.
+// Batch order (ordered): virtual wave vb of the grid-stride walk takes batch w.batch_order[...];
+// every wave records its batch's duration in w.batch_cost, from which launch_order_batches
+// prepares the next launch's order (longest first, so the deep reflection chains of a frame start
+// at once instead of trailing it). split (ordered stealing launches) = s2 | s4 << 16: the first s4
+// batches of the order run as four waves of 16 lanes each, the next s2 as two waves of 32, so the
+// other lanes of each are free to steal subtrees of the long walks from the start: virtual wave
+// vb < 4 s4 is quarter vb & 3 of batch order[vb >> 2]; then vb - 4 s4 < 2 s2 is half (vb - 4 s4) & 1
+// of batch order[s4 + ((vb - 4 s4) >> 1)]; later ones batch order[vb - 3 s4 - s2]. The host only
+// splits when a part holds whole pixels (launch_chain). Placement never changes results.
 template <int W, bool kAnyHit, bool kCount, bool kInLane = false, bool kSteal = false>
 __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kSteal ? RT_STEAL_WPE : RT_CHAIN_WPE))) void k_chain(
-    const DevScene sc, const ShadeParams p, DevWork w, int first, const Bvh4Node *__restrict__ n4,
-    const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx, int ordered, uint8_t *__restrict__ out_u8,
-    float *__restrict__ out_f32, int fuse_spp, const FrameGeom g, int split) {
-    constexpr bool kInlinePrimary = kInLane && RT_PRIMARY_INLINE;
+    const DevScene sc, const ShadeParams p, DevWork w, int first, int ordered, uint8_t *__restrict__ out_u8,
+    float *__restrict__ out_f32, int fuse_spp, int spb, int nbatch, const FrameGeom g, int split) {
     extern __shared__ int32_t lds_stack[];
     __shared__ int s_q[kChainSteps], s_sh[kChainSteps];
     for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) { s_q[i] = 0; s_sh[i] = 0; }
-#ifdef RT_REGION_COUNTS
-    if (threadIdx.x < 32) g_rc[threadIdx.x] = 0;
-#endif
     __syncthreads();
     const LaneStack stack = lane_stack(sc, lds_stack);
     WorkTally<kCount> wc, ws;   // closest-hit and shadow work (totals only: lanes diverge here)
-#ifdef RT_WAVE_TIMES   // diagnostic build: each wave's start / end clock (100 MHz) and query count
-    unsigned long long *wt_out = sc.work ? sc.work + 2 * kWorkFields + 3 * ((blockIdx.x * kBvhBlock + threadIdx.x) >> 6) : nullptr;
-    if (wt_out && (3 * ((blockIdx.x * kBvhBlock + threadIdx.x) >> 6) + 3 > kDiagWords)) wt_out = nullptr;
-    if (wt_out && __lane_id() == 0) wt_out[0] = __builtin_amdgcn_s_memrealtime();
-    unsigned long long wt_q = 0;
-#endif
-    const int nq = kInlinePrimary ? static_cast<int>(static_cast<int64_t>(g.ntiles) * g.tw * g.th * g.pfx * g.pfy)
-                                  : w.counters[first];
-    if (kInlinePrimary && w.counters_next) {   // k_gen_primary's resets, for the next launch (Pipe::cnt_buf)
+    const int nq = kInLane ? static_cast<int>(static_cast<int64_t>(g.ntiles) * g.tw * g.th * g.pfx * g.pfy)
+                           : w.counters[first];
+    if (kInLane && w.counters_next) {   // k_gen_primary's resets, for the next launch (Pipe::cnt_buf)
         const int i0 = blockIdx.x * kBvhBlock + threadIdx.x;   // (this launch's counters: already zero)
         for (int i = i0; i < 2 * kMaxStepsCounters; i += gridDim.x * kBvhBlock) w.counters_next[i] = 0;
         if (i0 == 0) w.counters[0] = nq;
     }
-    // split (ordered launches of the stealing kernel) = s2 | s4 << 16: the first s4 batches of the
-    // order (the longest) run as four waves of 16 samples each, the next s2 as two waves of 32, so
-    // the other lanes of each are free to steal subtrees of the long walks from the start. Virtual
-    // wave vb < 4 * s4 is quarter vb & 3 of batch order[vb >> 2]; then vb - 4 * s4 < 2 * s2 is half
-    // (vb - 4 * s4) & 1 of batch order[s4 + ((vb - 4 * s4) >> 1)]; later ones batch order[vb - extra]
+    if (!kInLane) nbatch = (nq + kWave - 1) / kWave;   // (spb = 64)
     const int s2 = split & 0xFFFF, s4 = split >> 16, extra = 3 * s4 + s2;
-    drive_queries(nq + extra * kWave, sc.chain_split & 3, w.wq + (2 * first) * kWqSlot, [&](int j0, int vend) {
-        const int end = vend - extra * kWave;
-        const int vb = j0 >> 6;   // this wave's batch in dispatch order (wave-uniform when ordered)
+    const int lane = __lane_id();
+    // pixel base lane of this lane's sample (fused launches): the first lane of its spp-lane group
+    const int pix_lane = kInLane ? ((fuse_spp & (fuse_spp - 1)) == 0 ? (lane & ~(fuse_spp - 1)) : lane - lane % fuse_spp) : 0;
+    drive_queries((nbatch + extra) * kWave, sc.chain_split & 3, w.wq + (2 * first) * kWqSlot, [&](int j0, int vend) {
+        const int vb = j0 >> 6;   // this wave's virtual batch (wave-uniform for the orderable distributions)
         const bool quarter = ordered && vb < 4 * s4;
         const bool half = ordered && !quarter && vb - 4 * s4 < 2 * s2;
         const int ob = quarter ? (vb >> 2) : half ? s4 + ((vb - 4 * s4) >> 1) : vb - (ordered ? extra : 0);
-        const int pb = (ordered && (vb << 6) < vend) ? w.batch_order[ob] : vb;
-        const int lane_off = quarter ? ((vb & 3) * (kWave / 4) + __lane_id())
-                           : half    ? (((vb - 4 * s4) & 1) * (kWave / 2) + __lane_id()) : (j0 & (kWave - 1));
-        const bool lane_on = quarter ? __lane_id() < kWave / 4 : !half || __lane_id() < kWave / 2;
+        const bool wave_on = (vb << 6) < vend;
+        const int pb = (ordered && wave_on) ? w.batch_order[ob] : vb;
+        const int lane_off = quarter ? ((vb & 3) * (kWave / 4) + lane)
+                           : half    ? (((vb - 4 * s4) & 1) * (kWave / 2) + lane) : (j0 & (kWave - 1));
+        // (unordered, the XCD-segment distributions hand out unaligned ranges: the lane's own bound)
+        const bool lane_on = (ordered ? wave_on : j0 < vend) && (quarter ? lane < kWave / 4 : !half || lane < kWave / 2) &&
+                             lane_off < spb;
+        const int j = pb * spb + lane_off;   // this lane's sample (kInLane) or queue entry
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         V3 rgb = mk(0, 0, 0);   // fused pixels: this lane's folded chain and its pixel (valid samples)
         int px = -1;
-        [&](int j) {
-        if (j >= end) return;
-        if (sc.chain_split & 4) j = nq - 1 - j;   // (diagnostic: reversed order)
+        [&]() {
+        if (!lane_on || j >= nq) return;
         V3 org, dst;
         int lvl, sample;
-        int64_t pxi = -1;
-        if (kInlinePrimary) {   // query j = sample j: its primary ray, as k_gen_primary makes it
+        if (kInLane) {   // sample j: its primary ray, as k_gen_primary makes it
+            int64_t pxi;
             int sub;
             if (!primary_sample(g, j, org, dst, pxi, sub)) {
                 if (g.out_mode == 0 && out_u8 && sub == 0) { out_u8[3 * pxi] = 0; out_u8[3 * pxi + 1] = 0; out_u8[3 * pxi + 2] = 0; }
                 return;
             }
+            px = static_cast<int>(pxi);
             lvl = 0;
             sample = j;
         } else {
@@ -2180,13 +1586,10 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
             org = mk(qo.x, qo.y, qo.z);
             dst = mk(qd.x, qd.y, qd.z);
         }
-#ifdef RT_WAVE_TIMES
-        ++wt_q;
-#endif
         for (int step = first; step < kChainSteps; ++step) {
             if (step > first) atomicAdd(&s_q[step], 1);
             const Secondary sec = chain_step<kAnyHit, W, kCount, kInLane, kSteal>(sc, p, w, step, sample, org, dst, lvl, stack,
-                                                                          lds_stack, n4, lrec, lidx, s_sh, wc, ws);
+                                                                                  s_sh, wc, ws);
             if (sec.state != kChildTrace) {
                 if (kInLane)   // the chain ends here: fold it in the lane (fold_chain's arithmetic)
                     rgb = fold_inlane(sc, w, first, step, sample,
@@ -2197,33 +1600,18 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
             dst = sec.dst;
             lvl = sec.lvl;
         }
-        if (fuse_spp) {
-            if (!kInLane) rgb = fold_chain(w, sample);
-            px = kInlinePrimary ? static_cast<int>(pxi) : w.pix_out[sample];
-        }
-        }(!lane_on ? end : ordered ? pb * kWave + lane_off : j0);
-        if (fuse_spp) {   // k_frame's arithmetic: a pixel's fuse_spp sub-samples sit in adjacent lanes
-            const int lane = __lane_id(), base = lane & ~(fuse_spp - 1);
+        }();
+        if (kInLane) {   // k_frame's arithmetic: a pixel's fuse_spp sub-samples sit in adjacent lanes
             V3 acc = mk(0, 0, 0);
             for (int sub = 0; sub < fuse_spp; ++sub)   // summed in sub-sample order (main.cpp:377-391)
-                acc = add(acc, mk(__shfl(rgb.x, base + sub), __shfl(rgb.y, base + sub), __shfl(rgb.z, base + sub)));
+                acc = add(acc, mk(__shfl(rgb.x, pix_lane + sub), __shfl(rgb.y, pix_lane + sub), __shfl(rgb.z, pix_lane + sub)));
             const float div = static_cast<float>(fuse_spp);
             acc = mk(acc.x / div, acc.y / div, acc.z / div);   // operator/, Vec3D.h:36-38
-            if (lane == base && px >= 0) store_pixel(acc, 3 * static_cast<int64_t>(px), out_u8, out_f32);
+            if (lane == pix_lane && px >= 0) store_pixel(acc, 3 * static_cast<int64_t>(px), out_u8, out_f32);
         }
-        if (__lane_id() == 0 && j0 < vend)
+        if (lane == 0 && wave_on)
             w.batch_cost[pb] = static_cast<uint32_t>(min(__builtin_amdgcn_s_memrealtime() - t0, 0xFFFFFFFFull));
     });
-#ifdef RT_WAVE_TIMES
-    for (int off = 32; off > 0; off >>= 1) wt_q += __shfl_xor(wt_q, off);
-    // HW_ID (hwreg 4): wave slot [3:0], SIMD [5:4], CU [11:8], SE [15:13] (gfx9 layout); XCC_ID (hwreg 20)
-    const unsigned hwid = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
-    const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));
-    if (wt_out && __lane_id() == 0) {
-        wt_out[1] = __builtin_amdgcn_s_memrealtime();
-        wt_out[2] = wt_q | (static_cast<unsigned long long>(hwid) << 32) | (static_cast<unsigned long long>(xcc & 0xF) << 60);
-    }
-#endif
     wc.flush(sc.work);
     ws.flush(sc.work ? sc.work + kWorkFields : nullptr);
     __syncthreads();
@@ -2231,133 +1619,6 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         if (s_q[i]) atomicAdd(&w.counters[i], s_q[i]);
         if (s_sh[i]) atomicAdd(&w.counters[kMaxStepsCounters + i], s_sh[i]);
     }
-#ifdef RT_REGION_COUNTS
-    if (threadIdx.x < 32 && sc.work && g_rc[threadIdx.x]) atomicAdd(&sc.work[2 * kWorkFields + threadIdx.x], g_rc[threadIdx.x]);
-#endif
-}
-
-// ---------------------------------------------------------------------------------------------
-// Chain launch with per-lane refill (RT_TUNE_CHAIN_REFILL 1; measured 1.5x slower than k_chain on C4
-// and 1.3x on C2, so not the default: mixing chain steps in a wave breaks the coherence of the
-// rays that k_chain's lanes trace side by side): a lane owns one pixel at a
-// time and runs its sub-samples' chains one after the other (main.cpp:377-391, summed in the same
-// order as k_frame); when the pixel is written it takes the next pixel from the wave's pool, which
-// the wave fills 64 pixels at a time from per-XCD work counters. Lanes no longer idle behind the
-// longest chain of a fixed 64-sample batch (k_chain: ~44% VALU lane utilisation on C4), and the
-// launch's tail is one pixel's chains rather than one batch's. Each step is chain_step, the same
-// arithmetic and record layout as k_chain, so results are identical; only placement changes.
-// ---------------------------------------------------------------------------------------------
-constexpr int kRefillChunk = 64;   // pixels per work-counter take (>= a wave's lanes)
-
-template <int W, bool kAnyHit, bool kCount>
-__global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(RT_CHAIN_WPE))) void k_chain_refill(
-    const DevScene sc, const ShadeParams p, DevWork w, const Bvh4Node *__restrict__ n4,
-    const TriRec *__restrict__ lrec, const uint32_t *__restrict__ lidx, uint8_t *__restrict__ out_u8,
-    float *__restrict__ out_f32, const FrameGeom g) {
-    extern __shared__ int32_t lds_stack[];
-    __shared__ int s_q[kChainSteps], s_sh[kChainSteps];
-    for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) { s_q[i] = 0; s_sh[i] = 0; }
-    __syncthreads();
-    const LaneStack stack = lane_stack(sc, lds_stack);
-    WorkTally<kCount> wc, ws;
-    const int spp = g.pfx * g.pfy;
-    const int npix = g.ntiles * g.tw * g.th;
-    const int lane = __lane_id();
-    const int home = blockIdx.x % kXcds;
-    int32_t *__restrict__ wq = w.wq;   // the step-0 chain slot: one counter per XCD (reset by k_gen_primary)
-    int pool = 0, pool_end = 0, xk = 0;   // wave-uniform: pixels [pool, pool_end) not handed out; counters tried
-    int pix = -1, sub = 0, step = 0, lvl = 0, sample = 0;
-    int64_t pxo = -1;
-    V3 acc = mk(0, 0, 0), org = mk(0, 0, 0), dst = mk(0, 0, 0);
-    // sample pix * spp + sub of this lane's pixel: its primary ray (false: outside the frame)
-    auto begin_sample = [&]() -> bool {
-        sample = pix * spp + sub;
-        int sub_out;
-        if (!primary_sample(g, sample, org, dst, pxo, sub_out)) return false;
-        step = 0;
-        lvl = 0;
-        return true;
-    };
-    while (true) {
-        // hand a pixel to every lane without one
-        const uint64_t idle = __ballot(pix < 0);
-        if (idle) {
-            const int nidle = __popcll(idle);
-            const int rank = __popcll(idle & ((1ull << lane) - 1ull));
-            const int avail = pool_end - pool;
-            int fresh = -1, fresh_len = 0;
-            while (avail < nidle && xk < kXcds) {   // take another chunk (own XCD first, then the others)
-                const int gx = (home + xk) % kXcds;
-                int c = 0;
-                if (lane == 0) c = atomicAdd(&wq[gx * kWqStride], 1);
-                c = __shfl(c, 0);
-                const int64_t start = (static_cast<int64_t>(c) * kXcds + gx) * kRefillChunk;
-                if (start < npix) {
-                    fresh = static_cast<int>(start);
-                    fresh_len = min(kRefillChunk, npix - fresh);
-                    break;
-                }
-                ++xk;
-            }
-            if (pix < 0) {
-                if (rank < avail) pix = pool + rank;
-                else if (rank - avail < fresh_len) pix = fresh + (rank - avail);
-            }
-            if (fresh >= 0) {
-                const int used = min(nidle - avail, fresh_len);
-                pool = fresh + used;
-                pool_end = fresh + fresh_len;
-            } else {
-                pool += min(nidle, avail);
-            }
-            if ((idle >> lane) & 1ull) {
-                if (pix >= 0) {
-                    sub = 0;
-                    acc = mk(0, 0, 0);
-                    if (!begin_sample()) {   // outside the frame: black in the tile-major layout (k_frame)
-                        if (g.out_mode == 0 && out_u8) { out_u8[3 * pxo] = 0; out_u8[3 * pxo + 1] = 0; out_u8[3 * pxo + 2] = 0; }
-                        pix = -1;
-                    }
-                }
-            }
-        }
-        if (!__ballot(pix >= 0)) {
-            if (xk >= kXcds && pool >= pool_end) break;   // every counter is spent and no lane has work
-            continue;
-        }
-        if (pix >= 0) {
-            if (step > 0) atomicAdd(&s_q[step], 1);
-            const Secondary sec = chain_step<kAnyHit, W, kCount, true>(sc, p, w, step, sample, org, dst, lvl, stack,
-                                                                      lds_stack, n4, lrec, lidx, s_sh, wc, ws);
-            if (sec.state != kChildTrace) {   // the chain ends: fold it (fold_chain's arithmetic)
-                const V3 rgb = fold_inlane(sc, w, 0, step, sample,
-                                           sec.state == kChildZero ? add(sec.local, mk(0.0f, 0.0f, 0.0f)) : sec.local);
-                acc = add(acc, rgb);   // sub-samples in order, from (0, 0, 0) (k_frame)
-                if (++sub == spp) {
-                    const float div = static_cast<float>(spp);
-                    store_pixel(mk(acc.x / div, acc.y / div, acc.z / div), 3 * pxo, out_u8, out_f32);   // operator/
-                    pix = -1;
-                } else {
-                    begin_sample();   // (same pixel: inside the frame)
-                }
-            } else {
-                org = sec.org;
-                dst = sec.dst;
-                lvl = sec.lvl;
-                ++step;
-            }
-        }
-    }
-    wc.flush(sc.work);
-    ws.flush(sc.work ? sc.work + kWorkFields : nullptr);
-    __syncthreads();
-    for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) {
-        if (s_q[i]) atomicAdd(&w.counters[i], s_q[i]);
-        if (s_sh[i]) atomicAdd(&w.counters[kMaxStepsCounters + i], s_sh[i]);
-    }
-#ifdef RT_REGION_COUNTS
-    if (threadIdx.x < 32 && sc.work && g_rc[threadIdx.x]) atomicAdd(&sc.work[2 * kWorkFields + threadIdx.x], g_rc[threadIdx.x]);
-#endif
 }
 
 // Frame: per pixel, sum sub-samples (subx outer, suby inner), divide by pf^2 (main.cpp:391),
@@ -2393,6 +1654,8 @@ __global__ __launch_bounds__(kBlock) void k_fold_rays(DevWork w, int32_t n, floa
 
 // Counting sort of the batches by duration, longest first: bucket = 4 x log2(ticks) plus the two
 // bits below the leading one (quarter-octave buckets); within a bucket the order is arbitrary.
+// (An order within eight screen bands, one per XCD, for L2 locality measured 40% slower: the bands'
+// unequal costs leave XCDs idle. DESIGN.md §7.)
 constexpr int kOrderBlock = 256;
 __device__ __forceinline__ int order_bucket(uint32_t c) {
     if (c < 4) return kOrderBuckets - 1;
@@ -2401,79 +1664,50 @@ __device__ __forceinline__ int order_bucket(uint32_t c) {
     return kOrderBuckets - 1 - min(k, kOrderBuckets - 1);   // descending duration
 }
 
-// XCD segments (segs == kXcds): dispatch slot v runs on XCD (v / 2) % 8 (two wave batches per
-// block, blocks dealt round-robin to the XCDs), so XCD x owns seg_count(n, x) of the n slots. (Measured
-// with 128-thread blocks; with 256 the segments are placement hints only, and the ordered launch's
-// batch mapping depends on this exact count, so it stays as measured.)
-// Segment x is that many consecutive batches in screen order and the sort runs within each
-// segment: each XCD's L2 then holds the geometry of one band of the screen, and within the band
-// the longest batches go first. Placement only; results never change.
-__device__ __forceinline__ int seg_count(int n, int x) { return 2 * (n / 16) + min(2, max(0, n % 16 - 2 * x)); }
-__device__ __forceinline__ int seg_of(int n, int i, int &start) {
-    int x = 0;
-    start = 0;
-    while (x < kXcds - 1 && i >= start + seg_count(n, x)) { start += seg_count(n, x); ++x; }
-    return x;
-}
-
-__global__ __launch_bounds__(kOrderBlock) void k_order_hist(const uint32_t *__restrict__ cost, int n, int segs,
-                                                         int32_t *hist) {
-    __shared__ int h[kOrderKeys];
-    const int nk = segs * kOrderBuckets;
-    for (int i = threadIdx.x; i < nk; i += kOrderBlock) h[i] = 0;
+__global__ __launch_bounds__(kOrderBlock) void k_order_hist(const uint32_t *__restrict__ cost, int n, int32_t *hist) {
+    __shared__ int h[kOrderBuckets];
+    for (int i = threadIdx.x; i < kOrderBuckets; i += kOrderBlock) h[i] = 0;
     __syncthreads();
-    for (int i = blockIdx.x * kOrderBlock + threadIdx.x; i < n; i += gridDim.x * kOrderBlock) {
-        int start = 0;
-        const int x = segs > 1 ? seg_of(n, i, start) : 0;
-        atomicAdd(&h[x * kOrderBuckets + order_bucket(cost[i])], 1);
-    }
+    for (int i = blockIdx.x * kOrderBlock + threadIdx.x; i < n; i += gridDim.x * kOrderBlock)
+        atomicAdd(&h[order_bucket(cost[i])], 1);
     __syncthreads();
-    for (int i = threadIdx.x; i < nk; i += kOrderBlock)
+    for (int i = threadIdx.x; i < kOrderBuckets; i += kOrderBlock)
         if (h[i]) atomicAdd(&hist[i], h[i]);
 }
 
-__global__ __launch_bounds__(kOrderKeys) void k_order_scan(int32_t *hist, int nk) {
-    __shared__ int h[kOrderKeys];
-    if (static_cast<int>(threadIdx.x) < nk) h[threadIdx.x] = hist[threadIdx.x];
+__global__ __launch_bounds__(kOrderBuckets) void k_order_scan(int32_t *hist) {
+    __shared__ int h[kOrderBuckets];
+    h[threadIdx.x] = hist[threadIdx.x];
     __syncthreads();
     if (threadIdx.x == 0) {
         int acc = 0;
-        for (int i = 0; i < nk; ++i) { const int c = h[i]; h[i] = acc; acc += c; }
+        for (int i = 0; i < kOrderBuckets; ++i) { const int c = h[i]; h[i] = acc; acc += c; }
     }
     __syncthreads();
-    if (static_cast<int>(threadIdx.x) < nk) hist[threadIdx.x] = h[threadIdx.x];   // key offsets; the scatter advances them
+    hist[threadIdx.x] = h[threadIdx.x];   // bucket offsets; the scatter advances them
 }
 
-__global__ __launch_bounds__(kOrderBlock) void k_order_scatter(const uint32_t *__restrict__ cost, int n, int segs,
-                                                            int32_t *offs, int32_t *__restrict__ order) {
-    __shared__ int h[kOrderKeys], base[kOrderKeys];
-    const int nk = segs * kOrderBuckets;
+__global__ __launch_bounds__(kOrderBlock) void k_order_scatter(const uint32_t *__restrict__ cost, int n, int32_t *offs,
+                                                            int32_t *__restrict__ order) {
+    __shared__ int h[kOrderBuckets], base[kOrderBuckets];
     for (int i0 = blockIdx.x * kOrderBlock; i0 < n; i0 += gridDim.x * kOrderBlock) {   // block-uniform
-        for (int i = threadIdx.x; i < nk; i += kOrderBlock) h[i] = 0;
+        for (int i = threadIdx.x; i < kOrderBuckets; i += kOrderBlock) h[i] = 0;
         __syncthreads();
         const int i = i0 + static_cast<int>(threadIdx.x);
-        int b = 0, r = 0, x = 0, start = 0;
+        int b = 0, r = 0;
         if (i < n) {
-            x = segs > 1 ? seg_of(n, i, start) : 0;
-            b = x * kOrderBuckets + order_bucket(cost[i]);
+            b = order_bucket(cost[i]);
             r = atomicAdd(&h[b], 1);
         }
         __syncthreads();
-        for (int k = threadIdx.x; k < nk; k += kOrderBlock)
+        for (int k = threadIdx.x; k < kOrderBuckets; k += kOrderBlock)
             if (h[k]) base[k] = atomicAdd(&offs[k], h[k]);
         __syncthreads();
-        if (i < n) {
-            const int pos = base[b] + r;
-            if (segs > 1) {   // rank within the segment -> the slot of that rank on the segment's XCD
-                const int rk = pos - start;
-                order[2 * (x + kXcds * (rk >> 1)) + (rk & 1)] = i;
-            } else {
-                order[pos] = i;
-            }
-        }
+        if (i < n) order[base[b] + r] = i;
         __syncthreads();
     }
 }
+
 
 // calculateNormals (raytracing.cpp:78-86) on the device, one lane per triangle:
 // normalize(crossProduct(v1 - v0, v2 - v0)) with Vec3D's operation order (Vec3D.h:142-151,185-191),
@@ -2565,8 +1799,6 @@ inline unsigned grid_for(int64_t n) { return static_cast<unsigned>((n + kBlock -
 
 }  // namespace
 
-bool primaries_inline() { return RT_CHAIN_INLANE && RT_PRIMARY_INLINE; }
-
 // The geometry's divisors as multiply-high magic numbers (fastdiv.h), for the kernels' index decoding.
 static FrameGeom with_divisors(FrameGeom g) {
     g.div_spp = make_udiv(static_cast<uint32_t>(g.pfx * g.pfy));
@@ -2578,13 +1810,12 @@ static FrameGeom with_divisors(FrameGeom g) {
     return g;
 }
 
-void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream, bool fused, uint8_t *out_u8) {
+void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream, bool resets_only) {
     const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th * g.pfx * g.pfy;
     if (n <= 0) return;
     const int64_t clear = std::max<int64_t>(2 * kMaxStepsCounters, 2 * static_cast<int64_t>(w.steps) * kWqSlot);
-    const bool inl = fused && primaries_inline();   // the chain launch makes the primaries: resets only
-    hipLaunchKernelGGL(k_gen_primary, dim3(grid_for(inl ? clear : std::max(n, clear))), dim3(kBlock), 0, stream,
-                       with_divisors(g), w, out_u8, inl ? 2 : fused ? 1 : 0);
+    hipLaunchKernelGGL(k_gen_primary, dim3(grid_for(resets_only ? clear : std::max(n, clear))), dim3(kBlock), 0, stream,
+                       with_divisors(g), w, resets_only ? 1 : 0);
 }
 
 void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevWork &w, hipStream_t stream) {
@@ -2602,7 +1833,7 @@ inline DevScene for_width(DevScene s, int W) {
     return s;
 }
 
-// 128-thread blocks with a 10-20 KB LDS stack: 16 resident per CU (32 waves) -> 4096 blocks.
+// Grid cap of the per-step BVH kernels (resident size at 7 waves per SIMD: a grid-stride walk).
 constexpr int kMaxBvhGrid = 4096;
 inline unsigned grid_bvh(int64_t n, int cap = kMaxBvhGrid) {
     return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n + kBvhBlock - 1) / kBvhBlock, cap)));
@@ -2610,35 +1841,20 @@ inline unsigned grid_bvh(int64_t n, int cap = kMaxBvhGrid) {
 inline unsigned grid_chunked(int64_t n) {
     return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n + kBlock * kPer - 1) / (kBlock * kPer), kMaxGrid)));
 }
-inline unsigned grid_stride(int64_t n) {
-    return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, kMaxGrid)));
-}
-
-// Tree kernel variant: 2 (binary, per lane), 4 (four-wide, per lane) or 5 (four-wide,
-// wave-coherent; DevScene::wave_mask bit `bit`).
-inline int tree_variant(const DevScene &s, int bit) {
-    if (s.bvh_width != 4) return 2;
-    return (bit >= 0 && ((static_cast<uint32_t>(s.wave_mask) >> bit) & 1u)) ? 5 : 4;
-}
-inline size_t tree_lds(const DevScene &s, int W) {
-    return W == 5 ? sizeof(int32_t) * (kBvhBlock / kWave) * static_cast<size_t>(std::max(s.bvh4_stack, 1)) : bvh_lds(s);
-}
 
 template <int W>
 void launch_ch(const DevScene &s0, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
     const DevScene s = for_width(s0, W);
     auto k = s.work ? k_bvh_closest_hit<W, true> : k_bvh_closest_hit<W, false>;
-    hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), tree_lds(s, W), stream, s,
+    hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s,
                        w.q_org[step & 1], w.q_dst[step & 1], &w.counters[step], w.hit_idx, w.hit_I,
-                       w.wq + (2 * step) * kWqSlot, s.nodes4, s.leaf_recs, s.leaf_idx);
+                       w.wq + (2 * step) * kWqSlot);
 }
 
 void launch_closest_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream) {
     if (capacity <= 0) return;
     if (s.use_bvh) {
-        const int W = tree_variant(s, std::min(step, 15));
-        if (W == 5) launch_ch<5>(s, w, step, capacity, stream);
-        else if (W == 4) launch_ch<4>(s, w, step, capacity, stream);
+        if (s.bvh_width == 4) launch_ch<4>(s, w, step, capacity, stream);
         else launch_ch<2>(s, w, step, capacity, stream);
         return;
     }
@@ -2658,8 +1874,8 @@ void launch_sh(const DevScene &s0, const DevWork &w, const ShadowSource &src, in
     const DevScene s = for_width(s0, W);
     auto k = s.any_transparent ? k_bvh_shadow_hit<false, W, false> : k_bvh_shadow_hit<true, W, false>;
     if (s.work) k = s.any_transparent ? k_bvh_shadow_hit<false, W, true> : k_bvh_shadow_hit<true, W, true>;
-    hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), tree_lds(s, W), stream, s, src, w.shadow,
-                       w.wq + (2 * step + 1) * kWqSlot, s.nodes4, s.leaf_recs, s.leaf_idx);
+    hipLaunchKernelGGL(k, dim3(grid_bvh(capacity, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, src, w.shadow,
+                       w.wq + (2 * step + 1) * kWqSlot);
 }
 
 void launch_shadow_hit(const DevScene &s, const DevWork &w, const ShadeParams &p, bool virt, int64_t capacity,
@@ -2678,9 +1894,7 @@ void launch_shadow_hit(const DevScene &s, const DevWork &w, const ShadeParams &p
     for (int l = 0; l < RT_MAX_LIGHTS; ++l)
         for (int k = 0; k < 3; ++k) src.lights[l][k] = p.lights[l][k];
     if (s.use_bvh) {
-        const int W = tree_variant(s, 16 + std::min(step, 15));
-        if (W == 5) launch_sh<5>(s, w, src, step, capacity, stream);
-        else if (W == 4) launch_sh<4>(s, w, src, step, capacity, stream);
+        if (s.bvh_width == 4) launch_sh<4>(s, w, src, step, capacity, stream);
         else launch_sh<2>(s, w, src, step, capacity, stream);
         return;
     }
@@ -2698,67 +1912,57 @@ void launch_shade(const DevScene &s, const DevWork &w, const ShadeParams &p, int
     hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kShadeBlock), 0, stream, s, p, w);
 }
 
+int chain_spb(int fuse_spp) { return fuse_spp > 0 && fuse_spp <= kWave ? (kWave / fuse_spp) * fuse_spp : kWave; }
+
+int64_t chain_batches(int64_t capacity, int fuse_spp) {
+    const int spb = chain_spb(fuse_spp);
+    return (capacity + spb - 1) / spb;
+}
+
+// k_chain's instantiations by width, any-hit shadows, work counting, fused frame and stealing
+typedef void (*ChainKernel)(const DevScene, const ShadeParams, DevWork, int, int, uint8_t *, float *, int, int, int,
+                            const FrameGeom, int);
+template <int W, bool kInLane, bool kSteal>
+ChainKernel chain_kernel(bool anyhit, bool count) {
+    return anyhit ? (count ? k_chain<W, true, true, kInLane, kSteal> : k_chain<W, true, false, kInLane, kSteal>)
+                  : (count ? k_chain<W, false, true, kInLane, kSteal> : k_chain<W, false, false, kInLane, kSteal>);
+}
+
 void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
                   hipStream_t stream, bool ordered, uint8_t *out_u8, float *out_f32, int fuse_spp, const FrameGeom *g) {
     if (capacity <= 0) return;
-    const bool wide = tree_variant(s0, -1) == 4;
+    const bool wide = s0.bvh_width == 4;
     const DevScene s = for_width(s0, wide ? 4 : 2);
-    auto k = wide ? (s.any_transparent ? k_chain<4, false, false> : k_chain<4, true, false>)
-                  : (s.any_transparent ? k_chain<2, false, false> : k_chain<2, true, false>);
-    // fused pixel writes from step 0: each lane folds its own chain (RT_CHAIN_INLANE)
-    const bool inlane = RT_CHAIN_INLANE && fuse_spp > 0 && first == 0 && g != nullptr;
-    if (inlane)
-        k = wide ? (s.any_transparent ? k_chain<4, false, false, true> : k_chain<4, true, false, true>)
-                 : (s.any_transparent ? k_chain<2, false, false, true> : k_chain<2, true, false, true>);
+    const bool anyhit = !s.any_transparent, count = s.work != nullptr;
+    // fused pixel writes from step 0: each lane makes its primary ray and folds its own chain
+    const bool fused = fuse_spp > 0 && fuse_spp <= kWave && first == 0 && g != nullptr;
     // in-wave work stealing (RT_TUNE_WAVE_STEAL; 2 = when the launch is at most two rounds of
-    // resident waves, where a few long walks set the frame time): four-wide, in-lane chains
-    const int64_t resident_lanes = static_cast<int64_t>(std::max(s.refill_grid, 1)) * kBvhBlock;
-    const bool steal = wide && inlane && (s.wave_steal == 1 || (s.wave_steal == 2 && capacity <= 2 * resident_lanes));
-    if (steal) k = s.any_transparent ? k_chain<4, false, false, true, true> : k_chain<4, true, false, true, true>;
-#if !defined(RT_WAVE_TIMES) && !defined(RT_REGION_COUNTS)   // (diagnostic builds run the uncounted kernel)
-    if (s.work && inlane && steal)
-        k = s.any_transparent ? k_chain<4, false, true, true, true> : k_chain<4, true, true, true, true>;
-    else if (s.work && inlane)
-        k = wide ? (s.any_transparent ? k_chain<4, false, true, true> : k_chain<4, true, true, true>)
-                 : (s.any_transparent ? k_chain<2, false, true, true> : k_chain<2, true, true, true>);
-    else if (s.work)
-        k = wide ? (s.any_transparent ? k_chain<4, false, true> : k_chain<4, true, true>)
-                 : (s.any_transparent ? k_chain<2, false, true> : k_chain<2, true, true>);
-#endif
-    const FrameGeom geom = g ? with_divisors(*g) : FrameGeom{};
-    if (inlane && chain_refill_used(s0, fuse_spp, g)) {
-        auto kr = wide ? (s.any_transparent ? k_chain_refill<4, false, false> : k_chain_refill<4, true, false>)
-                       : (s.any_transparent ? k_chain_refill<2, false, false> : k_chain_refill<2, true, false>);
-        if (s.work)
-            kr = wide ? (s.any_transparent ? k_chain_refill<4, false, true> : k_chain_refill<4, true, true>)
-                      : (s.any_transparent ? k_chain_refill<2, false, true> : k_chain_refill<2, true, true>);
-        // a resident grid: every wave keeps taking pixels until the counters are spent
-        const unsigned grid = std::min<unsigned>(grid_bvh(capacity, s.bvh_grid), static_cast<unsigned>(s.refill_grid));
-        hipLaunchKernelGGL(kr, dim3(grid), dim3(kBvhBlock), bvh_lds(s), stream, s, p, w, s.nodes4, s.leaf_recs,
-                           s.leaf_idx, out_u8, out_f32, geom);
-        return;
-    }
+    // resident waves, where a few long walks set the frame time): four-wide, fused launches
+    const int64_t resident_lanes = static_cast<int64_t>(std::max(s.resident_grid, 1)) * kBvhBlock;
+    const bool steal = wide && fused && (s.wave_steal == 1 || (s.wave_steal == 2 && capacity <= 2 * resident_lanes));
+    ChainKernel k = steal  ? chain_kernel<4, true, true>(anyhit, count)
+                  : fused  ? (wide ? chain_kernel<4, true, false>(anyhit, count) : chain_kernel<2, true, false>(anyhit, count))
+                           : (wide ? chain_kernel<4, false, false>(anyhit, count) : chain_kernel<2, false, false>(anyhit, count));
+    const int spb = fused ? chain_spb(fuse_spp) : kWave;
+    const int64_t nbatch = fused ? chain_batches(capacity, fuse_spp) : (capacity + kWave - 1) / kWave;
     // the stealing kernel, ordered over grid-stride batches: the longest batches run as quarter and
-    // half waves (at most 1/RT_STEAL_SPLIT_DIV of the batches together)
+    // half waves (at most 1/RT_STEAL_SPLIT_DIV of the batches together), when a part holds whole
+    // pixels (a pixel's sub-samples are summed within one wave's lanes)
     int s2 = 0, s4 = 0;
-    if (steal && ordered && (s.chain_split & 7) == 0) {
-        const int64_t cap = (capacity + kWave - 1) / kWave / RT_STEAL_SPLIT_DIV;
-        s4 = static_cast<int>(std::min<int64_t>(cap, s.steal_quarter));
-        s2 = static_cast<int>(std::min<int64_t>(cap - s4, s.steal_half));
+    if (steal && ordered && (s.chain_split & 3) == 0 && spb == kWave) {
+        const int64_t cap = nbatch / RT_STEAL_SPLIT_DIV;
+        if ((kWave / 4) % fuse_spp == 0) s4 = static_cast<int>(std::min<int64_t>(cap, s.steal_quarter));
+        if ((kWave / 2) % fuse_spp == 0) s2 = static_cast<int>(std::min<int64_t>(cap - s4, s.steal_half));
     }
     const int split = s2 | (s4 << 16);
-    hipLaunchKernelGGL(k, dim3(grid_bvh(capacity + static_cast<int64_t>(3 * s4 + s2) * kWave, s.bvh_grid)), dim3(kBvhBlock),
-                       bvh_lds(s), stream, s, p, w, first, s.nodes4, s.leaf_recs, s.leaf_idx, ordered ? 1 : 0, out_u8,
-                       out_f32, fuse_spp, geom, split);
+    const FrameGeom geom = g ? with_divisors(*g) : FrameGeom{};
+    hipLaunchKernelGGL(k, dim3(grid_bvh((nbatch + 3 * s4 + s2) * kWave, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s,
+                       p, w, first, ordered ? 1 : 0, out_u8, out_f32, fused ? fuse_spp : 0, spb, static_cast<int>(nbatch),
+                       geom, split);
 }
 
 int chain_blocks_per_cu() { return 4 * RT_CHAIN_WPE * kWave / kBvhBlock; }
 int bvh_block_threads() { return kBvhBlock; }
-
-bool chain_refill_used(const DevScene &s, int fuse_spp, const FrameGeom *g) {
-    return RT_CHAIN_INLANE && primaries_inline() && s.chain_refill && s.refill_grid > 0 && fuse_spp > 0 && g != nullptr &&
-           s.use_bvh;
-}
 
 void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream) {
     const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th;
@@ -2766,16 +1970,17 @@ void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *
     hipLaunchKernelGGL(k_frame, dim3(grid_for(n)), dim3(kBlock), 0, stream, with_divisors(g), w, out_u8, out_f32);
 }
 
-void launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream, bool xcd_segments) {
-    if (nbatches <= 0) return;
+hipError_t launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream) {
+    if (nbatches <= 0) return hipSuccess;
     const int n = static_cast<int>(nbatches);
-    const int segs = xcd_segments ? kXcds : 1, nk = segs * kOrderBuckets;
-    hipMemsetAsync(w.order_scratch, 0, sizeof(int32_t) * nk, stream);
+    const hipError_t e = hipMemsetAsync(w.order_scratch, 0, sizeof(int32_t) * kOrderBuckets, stream);
+    if (e != hipSuccess) return e;
     const unsigned grid = static_cast<unsigned>(std::min<int64_t>((nbatches + kOrderBlock - 1) / kOrderBlock, 1024));
-    hipLaunchKernelGGL(k_order_hist, dim3(grid), dim3(kOrderBlock), 0, stream, w.batch_cost, n, segs, w.order_scratch);
-    hipLaunchKernelGGL(k_order_scan, dim3(1), dim3(kOrderKeys), 0, stream, w.order_scratch, nk);
-    hipLaunchKernelGGL(k_order_scatter, dim3(grid), dim3(kOrderBlock), 0, stream, w.batch_cost, n, segs,
-                       w.order_scratch, w.batch_order);
+    hipLaunchKernelGGL(k_order_hist, dim3(grid), dim3(kOrderBlock), 0, stream, w.batch_cost, n, w.order_scratch);
+    hipLaunchKernelGGL(k_order_scan, dim3(1), dim3(kOrderBuckets), 0, stream, w.order_scratch);
+    hipLaunchKernelGGL(k_order_scatter, dim3(grid), dim3(kOrderBlock), 0, stream, w.batch_cost, n, w.order_scratch,
+                       w.batch_order);
+    return hipGetLastError();
 }
 
 void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t stream) {
@@ -2787,13 +1992,11 @@ void launch_intersect_only(const DevScene &s0, const float4 *org, const float4 *
                            float4 *I, hipStream_t stream) {
     if (n <= 0) return;
     if (s0.use_bvh) {
-        const int W = tree_variant(s0, 31);
+        const int W = s0.bvh_width == 4 ? 4 : 2;
         const DevScene s = for_width(s0, W);
-        auto k = W == 5 ? (s.work ? k_bvh_intersect_only<5, true> : k_bvh_intersect_only<5, false>)
-                 : W == 4 ? (s.work ? k_bvh_intersect_only<4, true> : k_bvh_intersect_only<4, false>)
-                          : (s.work ? k_bvh_intersect_only<2, true> : k_bvh_intersect_only<2, false>);
-        hipLaunchKernelGGL(k, dim3(grid_bvh(n, s.bvh_grid)), dim3(kBvhBlock), tree_lds(s, W), stream, s, org, dst, n, idx, I,
-                           s.nodes4, s.leaf_recs, s.leaf_idx);
+        auto k = W == 4 ? (s.work ? k_bvh_intersect_only<4, true> : k_bvh_intersect_only<4, false>)
+                        : (s.work ? k_bvh_intersect_only<2, true> : k_bvh_intersect_only<2, false>);
+        hipLaunchKernelGGL(k, dim3(grid_bvh(n, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s, org, dst, n, idx, I);
         return;
     }
     hipLaunchKernelGGL(k_intersect_only, dim3(grid_for(n)), dim3(kBlock), 0, stream, s0.tris, s0.nt, org, dst, n, idx, I);

@@ -93,13 +93,14 @@ def test_comm_id_without_gpu_and_init_refusal():
 
 def test_tune_knobs_validate_ranges(tmp_path):
     """rt_scene_tune range checks on a host-only scene (no GPU): the launch-shape knobs accept
-    their documented values and refuse others with RT_E_ARG."""
+    their documented values and refuse others with RT_E_ARG; the knobs retired in r03 (measured
+    slower, their kernels removed) accept only 0."""
     p = tmp_path / "t.obj"
     p.write_text("v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 3\n")
     s = R.Scene.load(str(p), device=R.RT_HOST_ONLY)
-    for knob, good, bad in [("wave_steal", (0, 1, 2), (-1, 3)), ("chain_refill", (0, 1), ()),
-                            ("refill_grid", (1, 2560), (0, 70000)), ("batch_order", (0, 1, 2), (3,)),
-                            ("chain_split", (0, 3, 7), (8,)),
+    for knob, good, bad in [("wave_steal", (0, 1, 2), (-1, 3)), ("chain_refill", (0,), (1,)),
+                            ("refill_grid", (0,), (1, 2560)), ("wave_traversal", (0,), (1, -1)),
+                            ("batch_order", (0, 1), (2, 3)), ("chain_split", (0, 3), (4, 7)),
                             ("steal_half", (0, 512, 65535), (-1, 65536)), ("steal_quarter", (0, 8, 4096), (-1, 4097)),
                             ("pipes", (1, 4), (0, 5))]:
         for v in good:
@@ -107,3 +108,37 @@ def test_tune_knobs_validate_ranges(tmp_path):
         for v in bad:
             with pytest.raises(R.RtError):
                 s.tune(knob, v)
+
+
+def _layout(cap, steps, lights):
+    total = C.c_uint64()
+    ext = (C.c_uint64 * (2 * _capi.RT_WS_ARRAYS))()
+    _capi.check(_capi.lib().rt_workspace_layout(cap, steps, lights, C.byref(total), ext))
+    return int(total.value), np.array(ext, dtype=np.uint64).reshape(-1, 2)
+
+
+@pytest.mark.parametrize("cap", [0, 1, 63, 64, 65, 1000, 4095, 2_073_600, 8_294_400 * 4])
+@pytest.mark.parametrize("steps", [1, 2, 4, 11, 255])
+@pytest.mark.parametrize("lights", [0, 1, 2, 4, 16])
+def test_workspace_layout_covers_every_array(cap, steps, lights):
+    """The render workspace (rt_capi.cpp layout_workspace) for every batch capacity the renderer
+    can ask for, max_lvl 0-254 and 0-16 lights: each array lies inside the allocation the library
+    makes (the sizing and the carving are one function; r02's abort was a carving that outgrew a
+    separately written size), no two arrays overlap, every array is 256-B aligned and holds what
+    the kernels index: queues c x 16 B, shadow pairs c x L, chain records c x steps x 16 B, the
+    counters 2 x 4096 words, the work-queue slots 2 x steps x 128 words, and the batch order/cost
+    arrays one entry per wave batch of the densest fused packing (>= 33 samples per batch: spp 33)."""
+    total, ext = _layout(cap, steps, lights)
+    L = max(lights, 1)
+    need = [cap * 16] * 4 + [cap * 4, cap * 16, cap * L * 16, cap * L * 16, cap * L, cap * steps * 16,
+                             cap * steps * 16, cap, 4 * 2 * 4096, 4 * 2 * 4096, 4 * 2 * steps * 128]
+    nbatch = max((cap + spb - 1) // spb for spb in [(64 // s) * s for s in range(1, 65)])
+    need += [4 * nbatch] * 4 + [4 * 128]
+    assert len(need) == _capi.RT_WS_ARRAYS
+    end = 0
+    for (off, size), n in zip(ext, need):
+        off, size = int(off), int(size)
+        assert off % 256 == 0 and off >= end, (off, end)
+        assert size >= n
+        end = off + size
+    assert end <= total

@@ -243,7 +243,7 @@ def _query_mix(sc, rng, n):
     return o, d
 
 
-@pytest.mark.parametrize("width", [2, 4, 5])
+@pytest.mark.parametrize("width", [2, 4])
 @pytest.mark.parametrize("spec", ["ref:dodgeColorTest.obj", "ref:Models/shadow_test.obj", "syn:F4", "syn:C4"])
 def test_bvh_matches_brute_force_bitwise(spec, width, workdir, gpu_available):
     path = scene_path(spec, workdir)
@@ -253,8 +253,7 @@ def test_bvh_matches_brute_force_bitwise(spec, width, workdir, gpu_available):
         sc.set_accel("brute_force")
         bi, bp = sc.intersect_mesh(o, d)
         sc.set_accel("bvh")
-        sc.tune("bvh_width", min(width, 4))
-        sc.tune("wave_traversal", -1 if width == 5 else 0)   # 5: the wave-coherent four-wide kernel
+        sc.tune("bvh_width", width)
         assert sc.accel() == "bvh"
         vi, vp = sc.intersect_mesh(o, d)
     assert np.array_equal(bi, vi), np.nonzero(bi != vi)[0][:10]
@@ -322,13 +321,12 @@ def test_c4_full_frame_bvh_equals_brute_force(workdir, gpu_available):
         assert np.array_equal(xf.view(np.uint32), bf.view(np.uint32))
 
 
-@pytest.mark.parametrize("mode,pf,size", [(1, 1, (320, 180)), (2, 1, (320, 180)), (2, 2, (200, 110)),
-                                          (2, 1, (37, 23))])
+@pytest.mark.parametrize("mode,pf,size", [(1, 1, (320, 180)), (1, 2, (200, 110)), (1, 1, (37, 23)), (1, 3, (90, 50))])
 def test_batch_order_from_previous_launch_keeps_results(mode, pf, size, workdir, gpu_available):
     """RT_TUNE_BATCH_ORDER: the first render dispatches the chain's batches in screen order and
-    times them; the next renders over the same batches dispatch them longest first (mode 2: within
-    one screen band per XCD, including frames of fewer than 16 batches). Every render is
-    byte-identical with identical ray counts, with the order on or off."""
+    times them; the next renders over the same batches dispatch them longest first (pf 3: 63-lane
+    batches of 7 pixels). Every render is byte-identical with identical ray counts, with the order
+    on or off."""
     p = R.RenderParams(width=size[0], height=size[1], pf=pf, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
     with R.Scene.load(scene_path("syn:C4", workdir), device=0) as sc:
         sc.tune("batch_order", 0)
@@ -373,17 +371,12 @@ def test_multi_frame_shard_batch_reassembles(workdir, gpu_available):
                                    {"bvh_width": 2, "xcd_split": 2}, {"lds_stack": 1}, {"lds_stack": 5, "bvh_grid": 7},
                                    {"bvh_width": 2, "lds_stack": 2}, {"pipes": 1}, {"pipes": 3},
                                    {"pipes": 4, "xcd_split": 2}, {"shadow_virtual": 0}, {"shadow_virtual": 5},
-                                   {"shadow_virtual": 0, "bvh_width": 2}, {"wave_traversal": 0},
-                                   {"wave_traversal": -1}, {"wave_traversal": -1, "shadow_virtual": 0},
-                                   {"wave_traversal": -1, "lds_stack": 1}, {"chain_from": 0}, {"chain_from": 1},
+                                   {"shadow_virtual": 0, "bvh_width": 2}, {"chain_from": 0}, {"chain_from": 1},
                                    {"chain_from": 3}, {"chain_from": 255}, {"chain_from": 0, "lds_stack": 1},
                                    {"chain_from": 1, "bvh_width": 2}, {"chain_from": 0, "pipes": 1},
                                    {"pipes": 2}, {"pipes": 2, "bvh_grid": 4096}, {"bvh_grid": 65536},
-                                   {"fuse_pixels": 0}, {"batch_order": 2}, {"batch_order": 2, "chain_split": 3},
-                                   {"chain_split": 1}, {"chain_split": 2}, {"chain_refill": 1},
-                                   {"chain_refill": 1, "batch_order": 0}, {"chain_refill": 1, "refill_grid": 1},
-                                   {"chain_refill": 1, "refill_grid": 3}, {"chain_refill": 1, "refill_grid": 7, "lds_stack": 1},
-                                   {"chain_refill": 1, "refill_grid": 5, "bvh_width": 2}, {"wave_steal": 0},
+                                   {"fuse_pixels": 0}, {"batch_order": 0}, {"batch_order": 0, "chain_split": 3},
+                                   {"chain_split": 1}, {"chain_split": 2}, {"chain_split": 3}, {"wave_steal": 0},
                                    {"wave_steal": 1}, {"wave_steal": 1, "lds_stack": 1},
                                    {"wave_steal": 1, "bvh_grid": 3}, {"wave_steal": 1, "top_nodes": 0}])
 def test_launch_shape_knobs_never_change_results(knobs, workdir, gpu_available):
@@ -422,15 +415,19 @@ def test_wave_steal_matches_plain_walk(spec, w, h, pf, lights, workdir, gpu_avai
             assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
 
 
-@pytest.mark.parametrize("spec,w,h,pf,half,quarter", [("ref:dodgeColorTest.obj", 400, 300, 1, 512, 8),
-                                                        ("ref:dodgeColorTest.obj", 200, 150, 1, 0, 4096),
-                                                        ("syn:C4", 160, 90, 2, 3, 5), ("syn:F4", 96, 54, 4, 0, 2)])
-def test_steal_split_matches_plain_walk(spec, w, h, pf, half, quarter, workdir, gpu_available):
+@pytest.mark.parametrize("spec,w,h,pf,pfy,half,quarter", [("ref:dodgeColorTest.obj", 400, 300, 1, 1, 512, 8),
+                                                            ("ref:dodgeColorTest.obj", 200, 150, 1, 1, 0, 4096),
+                                                            ("syn:C4", 160, 90, 2, 2, 3, 5), ("syn:F4", 96, 54, 4, 4, 0, 2),
+                                                            ("syn:C4", 64, 36, 8, 8, 512, 8), ("syn:C4", 80, 45, 4, 8, 512, 8),
+                                                            ("syn:F4", 60, 34, 3, 3, 512, 8), ("syn:C4", 72, 40, 2, 8, 8, 8)])
+def test_steal_split_matches_plain_walk(spec, w, h, pf, pfy, half, quarter, workdir, gpu_available):
     """RT_TUNE_STEAL_HALF / RT_TUNE_STEAL_QUARTER: in ordered launches of the stealing kernel the
-    longest batches run as four waves of 16 samples and the next as two of 32 (pf 2 and 4: a
-    pixel's sub-samples stay in adjacent lanes of one part). Frames, floats and ray counts equal the
-    plain walk's on every launch (the first is unordered, later ones ordered)."""
-    p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
+    longest batches run as four waves of 16 samples and the next as two of 32 when a part holds
+    whole pixels (pf 2 and 4: a pixel's sub-samples stay in adjacent lanes of one part); pf 8 x 8,
+    4 x 8 and 2 x 8 (64 and 32 and 16 sub-samples) and pf 3 (63-lane batches) must skip the parts
+    that would cut a pixel (a half-wave wrote half a pixel). Frames, floats and ray
+    counts equal the plain walk's on every launch (the first is unordered, later ones ordered)."""
+    p = R.RenderParams(width=w, height=h, pf=pf, pfy=pfy, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
     with R.Scene.load(scene_path(spec, workdir), device=0) as sc:
         sc.tune("wave_steal", 0)
         ref, reff, refc = sc.render(p, want_f32=True)
@@ -443,10 +440,12 @@ def test_steal_split_matches_plain_walk(spec, w, h, pf, half, quarter, workdir, 
             assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
 
 
-def test_wave_steal_auto_trials_keep_results(workdir, gpu_available):
+@pytest.mark.parametrize("w,h,pf", [(400, 300, 1), (64, 48, 8), (100, 75, 3)])
+def test_wave_steal_auto_trials_keep_results(w, h, pf, workdir, gpu_available):
     """RT_TUNE_WAVE_STEAL 2 (default): launches 2 and 3 over a frame geometry are timed without and
-    with stealing, later ones use the faster; every render of the sequence equals the plain walk's."""
-    p = R.RenderParams(width=400, height=300, pf=1, max_lvl=1, lights=[[0, 0, 4]])
+    with stealing, later ones use the faster; every render of the sequence equals the plain walk's
+    (pf 8: 64 sub-samples per pixel, where the half-wave split must stay off)."""
+    p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=1, lights=[[0, 0, 4]])
     with R.Scene.load(scene_path("ref:dodgeColorTest.obj", workdir), device=0) as sc:
         sc.tune("wave_steal", 0)
         ref, reff, refc = sc.render(p, want_f32=True)
@@ -457,26 +456,43 @@ def test_wave_steal_auto_trials_keep_results(workdir, gpu_available):
             assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
 
 
-@pytest.mark.parametrize("spec,w,h,pf,flags", [("syn:C4", 333, 187, 1, 0), ("syn:C4", 160, 90, 2, 0),
-                                               ("syn:F4", 96, 54, 3, 0), ("ref:dodgeColorTest.obj", 200, 150, 1, 0),
-                                               ("syn:F3", 70, 41, 2, 1 << 8), ("syn:F4", 17, 9, 1, 0)])
-def test_chain_refill_matches_fixed_batches(spec, w, h, pf, flags, workdir, gpu_available):
-    """RT_TUNE_CHAIN_REFILL 1: lanes take a new pixel when their pixel's chains end, so
-    chains of different samples and steps share a wave; every chain still runs chain_step on its own
-    sample, so frames (bytes and floats), ray counts and the tile-major device output equal the
-    fixed-batch launch's, with transparency (closest-hit shadows), pf 1-3 and jittered sampling."""
-    p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]],
+@pytest.mark.parametrize("spec,w,h,pf,pfy,flags", [("syn:C4", 333, 187, 3, 3, 0), ("syn:F4", 96, 54, 3, 3, 0),
+                                                   ("ref:dodgeColorTest.obj", 120, 90, 3, 3, 0), ("syn:F3", 70, 41, 3, 3, 1 << 8),
+                                                   ("syn:F4", 17, 9, 5, 5, 0), ("syn:C4", 50, 30, 3, 5, 0),
+                                                   ("syn:F4", 40, 22, 7, 9, 0)])
+def test_fused_packed_batches_match_frame_pass(spec, w, h, pf, pfy, flags, workdir, gpu_available):
+    """Sub-sample counts that do not divide 64 (the reference's default pf 3 x 3 = 9, main.cpp:377-391;
+    25, 15 and 63): the fused chain launch packs floor(64 / spp) whole pixels into each wave batch
+    (pf 3: 7 pixels x 9 sub-samples in 63 lanes) and sums each pixel's sub-samples by lane shuffles.
+    Frames (bytes and floats) and ray counts equal the unfused path's (chain records in HBM, then
+    k_frame), with transparency, jittered sampling, batch order and stealing on and off."""
+    p = R.RenderParams(width=w, height=h, pf=pf, pfy=pfy, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]],
                        flags=R.ALL_FEATURES | flags, seed=7)
     with R.Scene.load(scene_path(spec, workdir), device=0) as sc:
-        sc.tune("chain_refill", 0)
+        sc.tune("fuse_pixels", 0)
         ref, reff, refc = sc.render(p, want_f32=True)
-        sc.tune("chain_refill", 1)
-        for grid in (0, 2):
-            if grid:
-                sc.tune("refill_grid", grid)
-            u8, f32, c = sc.render(p, want_f32=True)
-            assert [int(x) for x in c] == [int(x) for x in refc]
-            assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
+        sc.tune("fuse_pixels", 1)
+        for steal in (0, 1, 2):
+            sc.tune("wave_steal", steal)
+            for _ in range(3):   # unordered, then ordered launches
+                u8, f32, c = sc.render(p, want_f32=True)
+                assert [int(x) for x in c] == [int(x) for x in refc]
+                assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
+
+
+@pytest.mark.parametrize("spec,w,h,pf", [("ref:dodgeColorTest.obj", 60, 45, 3), ("syn:F4", 48, 27, 3)])
+def test_fused_pf3_matches_oracle(spec, w, h, pf, workdir, gpu_available):
+    """The reference's default sub-sampling (pixelfactor 3, raytracing.cpp:23) through the fused
+    63-lane batches against the oracle at max_lvl 10 (raytracing.cpp:29): same ray counts, the
+    golden tests' byte and float bar."""
+    path = scene_path(spec, workdir)
+    lights = [(0.0, 0.0, 4.0)]
+    p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=10, lights=lights)
+    with R.Scene.load(path, device=0) as sc:
+        u8, f32, counts = sc.render(p, want_f32=True)
+    of32, ou8, ocounts = O.OracleScene(path).render(O.make_params(w, h, pf=pf, max_lvl=10, lights=lights), nthreads=16)
+    assert [int(c) for c in counts] == [int(c) for c in ocounts]
+    _assert_image_close(u8, f32, ou8, of32)
 
 
 @pytest.mark.parametrize("spec,w,h,pf", [("syn:F3", 128, 72, 2), ("syn:F4", 96, 54, 2), ("ref:dodgeColorTest.obj", 80, 60, 3)])
