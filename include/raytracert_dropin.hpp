@@ -1,38 +1,57 @@
 /* raytracert_dropin.hpp — source-level drop-in for the reference tracer's headers over librtamd.so.
  *
  * The reference's render path is declared in CG_Project/raytracing.h (globals and functions), with
- * its types in Vec3D.h, Vertex.h and mesh.h, and defined in raytracing.cpp + mesh.cpp. A host that
- * replaces
- *     #include "raytracing.h"          with          #include "raytracert_dropin.hpp"
- * and drops raytracing.cpp and mesh.cpp from its build compiles its main.cpp unchanged: the frame
- * loop of the 'r' key (main.cpp:340-411) keeps calling performRayTracing per sub-sample, and each
- * call runs on the GPU. For speed the whole loop collapses into one call, renderImage(), whose
- * clamped floats are exactly the loop's Image::_image (so writeImage produces the same PPM bytes).
+ * its types in Vec3D.h, Vertex.h and mesh.h, and defined in raytracing.cpp + mesh.cpp. A host
+ * (the reference's main.cpp) switches by editing its two includes, main.cpp:13-14,
+ *     #include "raytracing.h"  +  #include "mesh.h"      ->      #include "raytracert_dropin.hpp"
+ * (or, with no edit at all, by putting include/refcompat/ first on its include path: its
+ * raytracing.h, mesh.h, Vec3D.h and Vertex.h forward to this header), and by dropping
+ * raytracing.cpp and mesh.cpp from its build. Every reference-API call main.cpp makes then compiles
+ * and links against include/ + librtamd: MyMesh.draw() (main.cpp:179), yourDebugDraw() (:186),
+ * init() (:258), produceRay (defined by main.cpp, :300-325), the 'r' loop's performRayTracing per
+ * sub-sample and Vec3Df arithmetic (:355-395), yourKeyboardFunc() (:417). tests/cxx/dropin_main.cpp
+ * is such a host, written fresh against the reference interface.
  *
  *   reference                                   here
- *   template Vec3D<T>, Vec3Df (Vec3D.h)         Vec3D<T> with the same operators and operation order
- *   Vertex (Vertex.h), Triangle, Material,      the same members and accessors; Mesh::loadMesh
- *   Mesh (mesh.h:10-201)                        loads through librtamd (mesh.cpp semantics)
+ *   template Vec3D<T>, Vec3Df (Vec3D.h)         Vec3D<T> with the same members, operators and operation order
+ *   Vertex (Vertex.h), Triangle, Material,      the same members and accessors; Mesh::loadMesh loads
+ *   Mesh (mesh.h:10-201)                        through librtamd (mesh.cpp semantics); draw/drawSmooth
+ *                                               draw with GL when the host defines RTAMD_DROPIN_GL
  *   globals of raytracing.h:8-16                declared extern here, defined by the host's main.cpp
  *                                               as before (MyMesh, MyLightPositions, ...)
- *   globals of raytracing.cpp:15-36             defined here (inline): Ambient..Refraction,
- *                                               pixelfactorX/Y, max_lvl, normals
+ *   globals of raytracing.cpp:15-36             defined here (inline): Ambient..Refraction, WireFrame,
+ *                                               pixelfactorX/Y, max_lvl, normals (the debug-ray lists
+ *                                               and DebugMode live in namespace rtamd_dropin)
  *   init, calculateNormals, getMaterial,        same signatures and meaning; the ray functions run
  *   trace, performRayTracing, intersectMesh,    on the GPU scene built from MyMesh (uploadMesh())
- *   rayIntersectTriangle, isNullVector
+ *   rayIntersectTriangle, isNullVector,
+ *   yourDebugDraw, yourKeyboardFunc             the keys of raytracing.cpp:453-553 ('d' through
+ *                                               rt_debug_trace)
+ *
+ * performRayTracing and the 'r' loop: a call whose (origin, dest) is the first sub-sample of the
+ * loop main.cpp:369-388 runs for the current corner rays (produceRay) makes the header trace every
+ * sub-sample of that frame in one GPU call (rt_trace_rays over the loop's own rays, computed with
+ * the loop's own float expressions); the loop's later calls are answered from it while each
+ * (origin, dest) and every parameter the trace reads equal the prediction bit for bit, and any other
+ * call is traced on its own. The colours are those of the per-call path either way (the same
+ * rt_trace_rays arithmetic; tests/test_cxx_dropin.py checks both against the oracle); the unchanged
+ * loop just stops paying one GPU round trip per sub-sample (RTAMD_DROPIN_NO_FRAME_CACHE turns it off).
  *
  * Extra: RayTracerDevice (the GPU init() binds; RT_HOST_ONLY = loader only), uploadMesh() (re-upload
- * MyMesh after editing it), renderImage() (the 'r' loop in one call), performRayTracing over
- * vectors (batched). Failures throw rtamd_dropin::Error (the reference has no error path).
- * Not provided (GL preview only, no effect on the image): Mesh::draw/drawSmooth, yourDebugDraw,
- * the box/rectangle intersectors. Texture coordinates are not loaded (Mesh::texcoords stays
- * empty, Triangle::t = 0): the render path never reads them. Header-only; C++17; link -lrtamd.
+ * MyMesh after editing it), renderImage() (the 'r' loop in one call, Image::_image's floats),
+ * performRayTracing over vectors (batched). Failures throw rtamd_dropin::Error (the reference has no
+ * error path). Not provided (never called by main.cpp, no effect on the image): Mesh::loadMtl as a
+ * separate call (loadMesh loads the mtllib), the dead box/rectangle intersectors and getTeller
+ * (declared, never defined by the reference). Texture coordinates are not loaded (Mesh::texcoords
+ * stays empty, Triangle::t = 0): the render path never reads them. Header-only; C++17; -lrtamd.
  */
 #ifndef RAYTRACERT_DROPIN_HPP_
 #define RAYTRACERT_DROPIN_HPP_
 
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstring>
 #include <iostream>
 #include <map>
 #include <stdexcept>
@@ -49,7 +68,7 @@ class Vec3D {
     Vec3D() { p[0] = p[1] = p[2] = T(); }
     Vec3D(T x, T y, T z) { p[0] = x; p[1] = y; p[2] = z; }
     Vec3D(const Vec3D &o) { p[0] = o.p[0]; p[1] = o.p[1]; p[2] = o.p[2]; }
-    explicit Vec3D(T *q) { p[0] = q[0]; p[1] = q[1]; p[2] = q[2]; }
+    Vec3D(T *q) { p[0] = q[0]; p[1] = q[1]; p[2] = q[2]; }   // implicit, as Vec3D.h:70
     T &operator[](int i) { return p[i]; }
     const T &operator[](int i) const { return p[i]; }
     Vec3D &operator=(const Vec3D &o) { p[0] = o.p[0]; p[1] = o.p[1]; p[2] = o.p[2]; return *this; }
@@ -72,7 +91,50 @@ class Vec3D {
     }
     void fromTo(const Vec3D &a, const Vec3D &b) { for (int k = 0; k < 3; ++k) p[k] = b.p[k] - a.p[k]; }
     float transProduct(const Vec3D &v) const { return p[0] * v[0] + p[1] * v[1] + p[2] * v[2]; }
+    // two vectors orthogonal to this one (Vec3D.h:160-173): u from the smaller components, v = this x u
+    void getTwoOrthogonals(Vec3D &u, Vec3D &v) const {
+        if (std::fabs(p[0]) < std::fabs(p[1])) {
+            if (std::fabs(p[0]) < std::fabs(p[2])) u = Vec3D(0, -p[2], p[1]);
+            else u = Vec3D(-p[1], p[0], 0);
+        } else {
+            if (std::fabs(p[1]) < std::fabs(p[2])) u = Vec3D(p[2], 0, -p[0]);
+            else u = Vec3D(-p[1], p[0], 0);
+        }
+        v = crossProduct(*this, u);
+    }
     Vec3D projectOn(const Vec3D &N, const Vec3D &P) const { return *this - N * dotProduct(*this - P, N); }
+    // (length, angle with z, angle of the x-y projection with x) and back (Vec3D.h:212-243)
+    static Vec3D cartesianToPolar(const Vec3D &v) {
+        Vec3D polar;
+        polar[0] = v.getLength();
+        const T rxy = static_cast<T>(std::sqrt(v[0] * v[0] + v[1] * v[1]));
+        if (v[2] > 0.0f) polar[1] = static_cast<T>(std::atan(rxy / v[2]));
+        else if (v[2] < 0.0f) polar[1] = static_cast<T>(std::atan(rxy / v[2]) + M_PI);
+        else polar[1] = static_cast<T>(M_PI * 0.5f);
+        if (v[0] > 0.0f) polar[2] = static_cast<T>(std::atan(v[1] / v[0]));
+        else if (v[0] < 0.0f) polar[2] = static_cast<T>(std::atan(v[1] / v[0]) + M_PI);
+        else if (v[1] > 0) polar[2] = static_cast<T>(M_PI * 0.5f);
+        else polar[2] = static_cast<T>(-M_PI * 0.5);
+        return polar;
+    }
+    static Vec3D polarToCartesian(const Vec3D &v) {
+        return Vec3D(v[0] * static_cast<T>(std::sin(v[1])) * static_cast<T>(std::cos(v[2])),
+                     v[0] * static_cast<T>(std::sin(v[1])) * static_cast<T>(std::sin(v[2])), v[0] * static_cast<T>(std::cos(v[1])));
+    }
+    // this point in the frame (pos; u, v, n) (Vec3D.h:249-254)
+    Vec3D transformIn(const Vec3D &pos, const Vec3D &n, const Vec3D &u, const Vec3D &v) const {
+        const Vec3D q = *this - pos;
+        return Vec3D(u[0] * q[0] + u[1] * q[1] + u[2] * q[2], v[0] * q[0] + v[1] * q[1] + v[2] * q[2],
+                     n[0] * q[0] + n[1] * q[1] + n[2] * q[2]);
+    }
+    // "(x, y, z)" into buffer (the 'd' key prints it, raytracing.cpp:508-509). The reference's body is
+    // commented out (Vec3D.h:257), so it prints whatever the stack buffer held; this writes the text its
+    // comment intends.
+    char *toString(char *buffer, size_t size) const {
+        if (buffer && size) std::snprintf(buffer, size, "(%f, %f, %f)", static_cast<double>(p[0]), static_cast<double>(p[1]),
+                                          static_cast<double>(p[2]));
+        return buffer;
+    }
     T *pointer() { return p; }
     const T *pointer() const { return p; }
     static Vec3D segment(const Vec3D &a, const Vec3D &b) { return Vec3D(b[0] - a[0], b[1] - a[1], b[2] - a[2]); }
@@ -105,6 +167,7 @@ template <class T> bool operator<(const Vec3D<T> &a, const Vec3D<T> &b) { return
 template <class T> bool operator>=(const Vec3D<T> &a, const Vec3D<T> &b) { return a[0] >= b[0] || a[1] >= b[1] || a[2] >= b[2]; }
 template <class T> std::ostream &operator<<(std::ostream &o, const Vec3D<T> &v) { return o << v[0] << " " << v[1] << " " << v[2]; }
 template <class T> std::istream &operator>>(std::istream &i, Vec3D<T> &v) { return i >> v[0] >> v[1] >> v[2]; }
+template <class T> void swap(Vec3D<T> &a, Vec3D<T> &b) { const Vec3D<T> t = a; a = b; b = t; }   // Vec3D.h:275
 
 typedef Vec3D<float> Vec3Df;
 typedef Vec3D<double> Vec3Dd;
@@ -242,6 +305,36 @@ class Mesh {
         }
         for (Vertex &v : vertices) v.n.normalize();
     }
+    // the GL preview (mesh.cpp:53-90): flat (face normals) and smooth (vertex normals) shading, the
+    // triangle's Kd as colour. Immediate-mode GL when the host includes GL and defines
+    // RTAMD_DROPIN_GL; otherwise nothing (the render path never draws).
+    void draw() const {
+#ifdef RTAMD_DROPIN_GL
+        glBegin(GL_TRIANGLES);
+        for (size_t i = 0; i < triangles.size(); ++i) {
+            glColor3fv(materials.at(triangleMaterials.at(i)).Kd().pointer());
+            const Triangle &t = triangles[i];
+            Vec3Df n = Vec3Df::crossProduct(vertices[t.v[1]].p - vertices[t.v[0]].p, vertices[t.v[2]].p - vertices[t.v[0]].p);
+            n.normalize();
+            glNormal3f(n[0], n[1], n[2]);
+            for (int v = 0; v < 3; ++v) glVertex3fv(vertices[t.v[v]].p.pointer());
+        }
+        glEnd();
+#endif
+    }
+    void drawSmooth() const {
+#ifdef RTAMD_DROPIN_GL
+        glBegin(GL_TRIANGLES);
+        for (size_t i = 0; i < triangles.size(); ++i) {
+            glColor3fv(materials[triangleMaterials[i]].Kd().pointer());
+            for (int v = 0; v < 3; ++v) {
+                glNormal3fv(vertices[triangles[i].v[v]].n.pointer());
+                glVertex3fv(vertices[triangles[i].v[v]].p.pointer());
+            }
+        }
+        glEnd();
+#endif
+    }
     std::vector<Vertex> vertices;
     std::vector<Vec3Df> texcoords;
     std::vector<Triangle> triangles;
@@ -273,11 +366,24 @@ inline std::vector<Vec3Df> normals;   // per-triangle normals (calculateNormals)
 // the GPU init() binds (a HIP device index), or RT_HOST_ONLY: loader and getMaterial only
 inline int RayTracerDevice = 0;
 
+// raytracing.h:24 — "defined elsewhere" (main.cpp:322-325, over gluUnProject). Weak here: the 'r'
+// loop's frame cache and the 'd' key call it when the host defines it, and a host that never
+// does still links.
+void produceRay(int x_I, int y_I, Vec3Df &origin, Vec3Df &dest) __attribute__((weak));
+
 namespace rtamd_dropin {
 inline rt_scene *&scene() {
     static rt_scene *s = nullptr;
     return s;
 }
+inline uint64_t &scene_generation() {   // bumped by every uploadMesh()
+    static uint64_t g = 0;
+    return g;
+}
+// the ray debugger's state (raytracing.cpp:35-37: `o`, `d`, DebugMode; kept out of the global
+// namespace, where one-letter globals would collide with a host's names)
+inline bool DebugMode = false;
+inline std::vector<Vec3Df> debug_origins, debug_hits;
 inline rt_scene *need_scene() {
     if (!scene()) throw Error(RT_E_ARG, "no GPU scene: call init() (with RayTracerDevice a device index) first");
     return scene();
@@ -306,6 +412,7 @@ inline rt_params params(int levels_left) {
 inline void uploadMesh() {
     rt_scene_destroy(rtamd_dropin::scene());
     rtamd_dropin::scene() = nullptr;
+    ++rtamd_dropin::scene_generation();
     if (RayTracerDevice == RT_HOST_ONLY) return;
     std::vector<float> xyz;
     xyz.reserve(3 * MyMesh.vertices.size());
@@ -393,8 +500,114 @@ inline Vec3Df trace(const Vec3Df &origin, const Vec3Df &dest, int lvl) {
     return c;
 }
 
-// performRayTracing (raytracing.cpp:410-416)
-inline Vec3Df performRayTracing(const Vec3Df &origin, const Vec3Df &dest) { return trace(origin, dest, 0); }
+namespace rtamd_dropin {
+// Everything a trace reads besides the ray: the globals of raytracing.cpp/main.cpp and the scene.
+struct TraceState {
+    rt_scene *scene = nullptr;
+    uint64_t gen = 0;
+    bool amb = false, dif = false, refl = false, sha = false, spec = false, refr = false;
+    unsigned pfx = 0, pfy = 0, w = 0, h = 0;
+    int lvl = 0;
+    std::vector<Vec3Df> lights;
+    Vec3Df cam;
+    static TraceState now() {
+        TraceState t;
+        t.scene = rtamd_dropin::scene(); t.gen = scene_generation();
+        t.amb = Ambient; t.dif = Diffuse; t.refl = Reflection; t.sha = Shadows; t.spec = Specular; t.refr = Refraction;
+        t.pfx = pixelfactorX; t.pfy = pixelfactorY; t.w = WindowSize_X; t.h = WindowSize_Y;
+        t.lvl = max_lvl; t.lights = MyLightPositions; t.cam = MyCameraPosition;
+        return t;
+    }
+    bool operator==(const TraceState &o) const {   // (bitwise on the floats)
+        if (scene != o.scene || gen != o.gen || amb != o.amb || dif != o.dif || refl != o.refl || sha != o.sha ||
+            spec != o.spec || refr != o.refr || pfx != o.pfx || pfy != o.pfy || w != o.w || h != o.h || lvl != o.lvl ||
+            lights.size() != o.lights.size() || std::memcmp(cam.p, o.cam.p, sizeof cam.p) != 0)
+            return false;
+        return lights.empty() || std::memcmp(lights.data(), o.lights.data(), sizeof(Vec3Df) * lights.size()) == 0;
+    }
+    bool matches_globals() const {   // the same test against the live globals, without copying them
+        if (scene != rtamd_dropin::scene() || gen != scene_generation() || amb != Ambient || dif != Diffuse ||
+            refl != Reflection || sha != Shadows || spec != Specular || refr != Refraction || pfx != pixelfactorX ||
+            pfy != pixelfactorY || w != WindowSize_X || h != WindowSize_Y || lvl != max_lvl ||
+            lights.size() != MyLightPositions.size() || std::memcmp(cam.p, MyCameraPosition.p, sizeof cam.p) != 0)
+            return false;
+        return lights.empty() || std::memcmp(lights.data(), MyLightPositions.data(), sizeof(Vec3Df) * lights.size()) == 0;
+    }
+};
+
+inline bool same_bits(const Vec3Df &a, const Vec3Df &b) { return std::memcmp(a.p, b.p, sizeof a.p) == 0; }
+
+// The 'r' loop's sub-sample ray (main.cpp:380-386), with the loop's own expressions and types.
+inline void loop_ray(unsigned x, unsigned y, int subx, int suby, float divX, float divY, const Vec3Df *c, Vec3Df &origin,
+                     Vec3Df &dest) {
+    float xscale = 1.0f - (float(x) * pixelfactorX + subx) / divX;
+    float yscale = 1.0f - (float(y) * pixelfactorY + suby) / divY;
+    origin = yscale * (xscale * c[0] + (1 - xscale) * c[4]) + (1 - yscale) * (xscale * c[2] + (1 - xscale) * c[6]);
+    dest = yscale * (xscale * c[1] + (1 - xscale) * c[5]) + (1 - yscale) * (xscale * c[3] + (1 - xscale) * c[7]);
+}
+
+// Every sub-sample colour of one 'r' frame, in the loop's call order (y, x, subx, suby).
+struct FrameCache {
+    TraceState state;
+    std::vector<Vec3Df> org, dst, rgb;
+    size_t next = 0;
+};
+inline FrameCache &frame_cache() {
+    static FrameCache c;
+    return c;
+}
+
+// If (origin, dest) is the first sub-sample of the 'r' loop for the current corner rays, trace the
+// whole frame's sub-samples in one GPU call (chunks of 2^22 rays) into the cache and return true.
+inline bool start_frame(const Vec3Df &origin, const Vec3Df &dest) {
+    if (!produceRay || WindowSize_X == 0 || WindowSize_Y == 0 || pixelfactorX == 0 || pixelfactorY == 0 || !scene())
+        return false;
+    Vec3Df c[8];   // origin00, dest00, origin01, dest01, origin10, dest10, origin11, dest11 (main.cpp:355-358)
+    produceRay(0, 0, c[0], c[1]);
+    float divX = (WindowSize_X * pixelfactorX - 1);
+    float divY = (WindowSize_Y * pixelfactorY - 1);
+    Vec3Df o0, d0;
+    produceRay(0, WindowSize_Y - 1, c[2], c[3]);
+    produceRay(WindowSize_X - 1, 0, c[4], c[5]);
+    produceRay(WindowSize_X - 1, WindowSize_Y - 1, c[6], c[7]);
+    loop_ray(0, 0, 0, 0, divX, divY, c, o0, d0);
+    if (!same_bits(o0, origin) || !same_bits(d0, dest)) return false;
+    const size_t n = static_cast<size_t>(WindowSize_X) * WindowSize_Y * pixelfactorX * pixelfactorY;
+    FrameCache &fc = frame_cache();
+    fc.org.resize(n);
+    fc.dst.resize(n);
+    fc.rgb.resize(n);
+    size_t k = 0;
+    for (unsigned int y = 0; y < WindowSize_Y; ++y)
+        for (unsigned int x = 0; x < WindowSize_X; ++x)
+            for (int subx = 0; subx < static_cast<int>(pixelfactorX); subx++)
+                for (int suby = 0; suby < static_cast<int>(pixelfactorY); suby++, ++k)
+                    loop_ray(x, y, subx, suby, divX, divY, c, fc.org[k], fc.dst[k]);
+    const rt_params p = params(max_lvl);
+    constexpr size_t kChunk = size_t(1) << 22;
+    for (size_t b = 0; b < n; b += kChunk) {
+        const int32_t m = static_cast<int32_t>(std::min(kChunk, n - b));
+        check(rt_trace_rays(scene(), &p, fc.org[b].p, fc.dst[b].p, m, fc.rgb[b].p, nullptr));
+    }
+    fc.state = TraceState::now();
+    fc.next = 0;
+    return true;
+}
+}  // namespace rtamd_dropin
+
+// performRayTracing (raytracing.cpp:410-416). The sub-samples of an 'r' loop come from the frame
+// cache (see the top of this file); any other ray is traced on its own. Same colours either way.
+inline Vec3Df performRayTracing(const Vec3Df &origin, const Vec3Df &dest) {
+#ifndef RTAMD_DROPIN_NO_FRAME_CACHE
+    using namespace rtamd_dropin;
+    FrameCache &fc = frame_cache();
+    if (fc.next < fc.org.size() && same_bits(origin, fc.org[fc.next]) && same_bits(dest, fc.dst[fc.next]) &&
+        fc.state.matches_globals())
+        return fc.rgb[fc.next++];
+    if (start_frame(origin, dest)) return fc.rgb[fc.next++];
+#endif
+    return trace(origin, dest, 0);
+}
 
 // the same for many rays in one GPU call
 inline std::vector<Vec3Df> performRayTracing(const std::vector<Vec3Df> &origins, const std::vector<Vec3Df> &dests) {
@@ -420,6 +633,102 @@ inline std::vector<float> renderImage(const Vec3Df &origin00, const Vec3Df &dest
     std::vector<float> img(3u * WindowSize_X * WindowSize_Y);
     rtamd_dropin::check(rt_render_tile(rtamd_dropin::need_scene(), &p, 0, 0, p.width, p.height, nullptr, img.data(), rays));
     return img;
+}
+
+// yourDebugDraw (raytracing.cpp:434-451): the debug rays (origin red -> hit green) and light 0 as
+// a point, with GL when the host defines RTAMD_DROPIN_GL; otherwise nothing (no effect on the image).
+inline void yourDebugDraw() {
+#ifdef RTAMD_DROPIN_GL
+    glPushAttrib(GL_ALL_ATTRIB_BITS);
+    glDisable(GL_LIGHTING);
+    glBegin(GL_LINES);
+    for (size_t i = 0; i < rtamd_dropin::debug_origins.size(); ++i) {
+        glColor3f(1, 0, 0);
+        glVertex3fv(rtamd_dropin::debug_origins[i].pointer());
+        glColor3f(0, 1, 0);
+        glVertex3fv(rtamd_dropin::debug_hits[i].pointer());
+    }
+    glEnd();
+    glPointSize(10);
+    glBegin(GL_POINTS);
+    if (!MyLightPositions.empty()) glVertex3fv(MyLightPositions[0].pointer());
+    glEnd();
+    glPopAttrib();
+#endif
+}
+
+// yourKeyboardFunc (raytracing.cpp:453-553): '1'-'6' toggle Ambient, Diffuse, Specular, Reflection,
+// Shadows, Refraction; '+'/'-' step both pixel factors (clamped at 1); '0' toggles the ray debugger;
+// 'd' (debugger on) shoots the ray through the mouse position (produceRay), records (origin, first
+// hit) and prints the ray's colour, through rt_debug_trace (the per-bounce records of trace());
+// 'c' clears the recorded rays; 'w' toggles wire frame. Then the settings, as the reference prints them.
+inline void yourKeyboardFunc(char key, int x, int y) {
+    using rtamd_dropin::DebugMode;
+    switch (key) {
+        case '1': Ambient = !Ambient; break;
+        case '2': Diffuse = !Diffuse; break;
+        case '3': Specular = !Specular; break;
+        case '4': Reflection = !Reflection; break;
+        case '5': Shadows = !Shadows; break;
+        case '6': Refraction = !Refraction; break;
+        case '+':
+            pixelfactorX++;
+            pixelfactorY++;
+            break;
+        case '-':
+            pixelfactorX--;
+            pixelfactorY--;
+            if (pixelfactorX < 1) pixelfactorX = 1;
+            if (pixelfactorY < 1) pixelfactorY = 1;
+            break;
+        case '0':
+            DebugMode = !DebugMode;
+            std::cout << "Debug Mode:\n 0 to enable / disable debug mode\n d to shoot & draw a ray trace.\n c to clear ray trace history.\n";
+            break;
+        case 'd':
+            if (DebugMode && produceRay) {
+                Vec3Df origin, dest;
+                produceRay(x, y, origin, dest);
+                const rt_params p = rtamd_dropin::params(max_lvl);
+                rt_debug_bounce b[1];
+                int32_t nb = 0;
+                Vec3Df color;
+                rtamd_dropin::check(rt_debug_trace(rtamd_dropin::need_scene(), &p, origin.p, dest.p, b, 1, &nb, color.p));
+                // intersectMesh's point (raytracing.cpp:498-502): the first bounce's hit, (0,0,0) on a miss
+                rtamd_dropin::debug_origins.push_back(origin);
+                rtamd_dropin::debug_hits.push_back(nb > 0 && b[0].triangle >= 0 ? Vec3Df(b[0].hit[0], b[0].hit[1], b[0].hit[2])
+                                                                               : Vec3Df(0, 0, 0));
+                char buffer[128];
+                std::cout << "Ray trace color = " << color.toString(buffer, sizeof(buffer)) << std::endl;
+            }
+            return;
+        case 'c':
+            rtamd_dropin::debug_origins.clear();
+            rtamd_dropin::debug_hits.clear();
+            std::cout << "Ray trace history cleared\n";
+            return;
+        case 'w':
+            WireFrame = !WireFrame;
+#ifdef RTAMD_DROPIN_GL
+            glPolygonMode(GL_FRONT_AND_BACK, WireFrame ? GL_LINE : GL_FILL);
+#endif
+            std::cout << (WireFrame ? "WireFrame enabled\n" : "WireFrame disabled\n");
+            break;
+        default: break;
+    }
+    std::cout << std::endl << "------SETTINGS------" << std::endl
+              << "Ammbient " << (Ambient ? "ON" : "OFF") << std::endl
+              << "Diffuse " << (Diffuse ? "ON" : "OFF") << std::endl
+              << "Specular " << (Specular ? "ON" : "OFF") << std::endl
+              << "Reflection " << (Reflection ? "ON" : "OFF") << std::endl
+              << "Shadow " << (Shadows ? "ON" : "OFF") << std::endl
+              << "Refraction " << (Refraction ? "ON" : "OFF") << std::endl
+              << "pixelfactorX = " << pixelfactorX << std::endl
+              << "pixelfactorY = " << pixelfactorY << std::endl
+              << "DebugMode " << (DebugMode ? "ON" : "OFF") << std::endl
+              << "WireFrame " << (WireFrame ? "ON" : "OFF") << std::endl
+              << "--------------------" << std::endl;
+    std::cout << " pressed! The mouse was in location " << x << "," << y << "!" << std::endl;
 }
 
 #endif  // RAYTRACERT_DROPIN_HPP_

@@ -1,0 +1,5 @@
+/* include/refcompat/mesh.h — forwards the reference's CG_Project/mesh.h to the MI355X drop-in, so a host
+ * whose sources include "mesh.h" compiles unchanged when this directory replaces the reference's
+ * headers (see include/raytracert_dropin.hpp and INTEGRATION.md). */
+#pragma once
+#include "../raytracert_dropin.hpp"

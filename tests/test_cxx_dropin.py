@@ -1,9 +1,11 @@
 """include/raytracert_dropin.hpp, the source-level drop-in for the reference's raytracing.h /
-mesh.h / Vec3D.h: tests/cxx/dropin_frame.cpp is written against the reference interface (its
-globals defined as main.cpp defines them, the 'r' key's loop restated) and compiles with g++
-against include/ unchanged. Host mode checks the loader's MyMesh, normals and getMaterial against
-the oracle; GPU mode checks that the per-sub-sample performRayTracing loop, the one-call
-renderImage and the oracle produce the same image."""
+mesh.h / Vec3D.h: tests/cxx/dropin_main.cpp is a host written fresh against the reference interface
+the way CG_Project/main.cpp uses it (its globals, RGBValue/Image, produceRay, the 'r' loop with one
+performRayTracing per sub-sample, keyboard() ending in yourKeyboardFunc, MyMesh.draw() and
+yourDebugDraw() from the draw function). It compiles with g++ against include/ only. Host mode checks
+the loader's MyMesh, normals and getMaterial against the oracle; GPU mode replays a key session
+(feature toggles '1'-'6', pixel factor '+'/'-', 'L' lights, the debugger's '0'/'d'/'c', 'r' frames)
+and checks every frame and every 'd' colour against the oracle with the same settings."""
 import os
 import subprocess
 
@@ -14,26 +16,33 @@ import oracle as O
 from _util import read_ppm, scene_path
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+F32_TOL = 2e-6
 
 
-@pytest.fixture(scope="module")
-def dropin_bin(tmp_path_factory):
-    out = str(tmp_path_factory.mktemp("dropin") / "dropin_frame")
+def _build(out, extra):
     lib = os.path.join(ROOT, "raytracert_amd")
-    cmd = ["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-Wall", "-Werror", "-I" + os.path.join(ROOT, "include"),
-           os.path.join(ROOT, "tests", "cxx", "dropin_frame.cpp"), "-L" + lib, "-lrtamd", "-Wl,-rpath," + lib, "-o", out]
+    cmd = ["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-Wall", "-Werror"] + extra + [
+        os.path.join(ROOT, "tests", "cxx", "dropin_main.cpp"), "-L" + lib, "-lrtamd", "-Wl,-rpath," + lib, "-o", out]
     subprocess.run(cmd, check=True)
     return out
 
 
-def _run(args):
+@pytest.fixture(scope="module")
+def dropin_bin(tmp_path_factory):
+    return _build(str(tmp_path_factory.mktemp("dropin") / "dropin_main"), ["-I" + os.path.join(ROOT, "include")])
+
+
+def test_dropin_refcompat_headers_compile_unchanged_includes(tmp_path, workdir):
+    """The no-edit route: main.cpp's own `#include "raytracing.h"` / `#include "mesh.h"` with
+    include/refcompat on the include path (its four headers forward to the drop-in)."""
+    exe = _build(str(tmp_path / "dropin_refcompat"), ["-DRTAMD_REFCOMPAT", "-I" + os.path.join(ROOT, "include", "refcompat")])
+    lines = _lines([exe, "host", scene_path("ref:cube.obj", workdir)])
+    assert lines[0].startswith("mesh 8 12 12 ")
+
+
+def _lines(args):
     r = subprocess.run(args, check=True, capture_output=True, text=True, timeout=600)
-    out = {}
-    for l in r.stdout.splitlines():   # first line of each kind; "material" lines are kept in order
-        out.setdefault(l.split()[0], l.split()[1:])
-        if l.startswith("material"):
-            out.setdefault("materials", []).append(l.split()[1:])
-    return out
+    return r.stdout.splitlines()
 
 
 def _fnv(words):
@@ -50,35 +59,97 @@ def _bits(x):
 @pytest.mark.parametrize("spec", ["ref:dodgeColorTest.obj", "ref:cube.obj", "syn:F4"])
 def test_dropin_host_mesh_matches_oracle(spec, dropin_bin, workdir):
     path = scene_path(spec, workdir)
-    out = _run([dropin_bin, "host", path])
+    lines = _lines([dropin_bin, "host", path])
+    out = {}
+    for l in lines:
+        out.setdefault(l.split()[0], l.split()[1:])
+    mats = [l.split()[1:] for l in lines if l.startswith("material")]
     e = O.OracleScene(path).export()
     V, F, tm, N = e["vertices"], e["triangles"], e["tri_mat"], e["normals"]
     assert out["mesh"][:4] == [str(len(V)), str(len(F)), str(len(F)), str(len(e["materials"]))]
     assert out["mesh"][5] == "1" and out["mesh"][7] == str(len(F))          # light 0, one normal per triangle
     tri_words = np.concatenate([F, tm[:, None]], 1).reshape(-1)
     assert out["digest"] == [_fnv(V.reshape(-1).view(np.uint32)), _fnv(N.reshape(-1).view(np.uint32)), _fnv(tri_words)]
-    for line, t in zip(out["materials"], (0, len(F) - 1)):
+    for line, t in zip(mats, (0, len(F) - 1)):
         m = e["materials"][tm[t]]
         assert line[0] == str(t)
         assert line[1:4] == [_bits(v) for v in m["Kd"]] and line[4] == _bits(m["Ks"][0])
         assert line[5] == _bits(m["Ns"]) and line[6] == _bits(m["Tr"]) and line[7] == str(m["illum"])
+    # Vec3D.h API: getTwoOrthogonals gives vectors orthogonal to the input; toString's text
+    assert abs(float(out["vec"][0])) < 1e-6 and abs(float(out["vec"][1])) < 1e-6
+    assert " ".join(out["vec"][2:]) == "(1.000000, 2.000000, 3.000000)"
+
+
+def _flags(s):
+    return sum(1 << i for i, c in enumerate(s) if c == "1")   # Ambient Diffuse Specular Reflection Shadows Refraction
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("spec,w,h,pf,lvl", [("syn:F4", 40, 24, 2, 3), ("ref:dodgeColorTest.obj", 48, 36, 1, 1)])
-def test_dropin_frame_loop_equals_render_and_oracle(spec, w, h, pf, lvl, dropin_bin, workdir, tmp_path, gpu_available):
+@pytest.mark.parametrize("spec,w,h", [("syn:F4", 40, 24), ("ref:dodgeColorTest.obj", 48, 36)])
+def test_dropin_key_session_matches_oracle(spec, w, h, dropin_bin, workdir, tmp_path, gpu_available):
+    """A main.cpp-style session through yourKeyboardFunc (raytracing.cpp:453-553): the default
+    frame (pf 3, max_lvl 10, light 0 = camera), then ambient off, shadows off, pf 4 and back down to
+    2 (clamped at 1 below), a second light ('L'), reflection and refraction off, each rendered by the
+    unchanged 'r' loop (one performRayTracing per sub-sample), plus renderImage() once; the debugger
+    ('0', 'd' at two mouse positions, 'c'). Every frame equals the oracle's at the settings the
+    session printed (same bar as the golden tests), the one-call frame equals the loop's, and each
+    'd' prints the oracle's colour of the ray produceRay shot."""
     path = scene_path(spec, workdir)
-    loop_ppm, fast_ppm = str(tmp_path / "loop.ppm"), str(tmp_path / "fast.ppm")
-    out = _run([dropin_bin, "gpu", path, str(w), str(h), str(pf), str(lvl), loop_ppm, fast_ppm])
-    assert out["frames"][0] == out["frames"][1] == str(w * h * 3)      # loop floats == renderImage floats, bit for bit
-    a, b = read_ppm(loop_ppm), read_ppm(fast_ppm)
-    assert np.array_equal(a, b)
-    lights = [(0.0, 0.0, 4.0), (1.5, 1.5, 4.0)]
-    _, ou8, oc = O.OracleScene(path).render(O.make_params(w, h, pf, lvl, lights=lights), nthreads=16)
-    d = np.abs(a.astype(np.int16) - ou8.astype(np.int16))
-    assert d.max() <= 1 and (d == 0).mean() >= 0.9999
-    assert out["frames"][2] == "rays" and out["frames"][3:6] == [str(int(x)) for x in oc]
-    c = out["centre"]   # idx, I (3 words), "tri_hit", hit, "same_point", same
-    assert c[4] == "tri_hit" and c[6] == "same_point"
-    if c[0] != "-1":   # rayIntersectTriangle on intersectMesh's triangle: a hit at the same point
-        assert c[5] == "1" and c[7] == "1"
+    prefix = str(tmp_path / "f")
+    keys = ["r", "1", "r", "1", "5", "r", "+", "r", "-", "-", "r", "-", "-", "r", "+", "L", "r", "4", "6", "r", "R",
+            "0", "d@5,7", "d@20,11", "c", "5", "r"]
+    lines = _lines([dropin_bin, "keys", path, str(w), str(h), prefix] + keys)
+    frames = [l.split() for l in lines if l.startswith("frame ")]
+    assert len(frames) == keys.count("r") + keys.count("R")
+    orc = O.OracleScene(path)
+    cache = {}
+    expect_pf = [3, 3, 3, 4, 2, 1, 2, 2, 2, 2]
+    lights_n = [1, 1, 1, 1, 1, 1, 2, 2, 2, 2]
+    for i, f in enumerate(frames):
+        pfx, pfy = int(f[3]), int(f[4])
+        assert pfx == pfy == expect_pf[i]
+        if f[5] == "renderImage":
+            flags, nl = cache["last"]
+        else:
+            flags, nl = _flags(f[6]), int(f[8])
+            cache["last"] = (flags, nl)
+        assert nl == lights_n[i]
+        img = read_ppm(f[1])
+        key = (pfx, flags, nl)
+        if key not in cache:
+            lights = [(0.0, 0.0, 4.0)] * nl
+            cache[key] = orc.render(O.make_params(w, h, pf=pfx, max_lvl=10, lights=lights, flags=flags), nthreads=16)[1]
+        d = np.abs(img.astype(np.int16) - cache[key].astype(np.int16))
+        assert d.max() <= 1 and (d == 0).mean() >= 0.9999, (i, f)
+    # the one-call frame ('R') is the frame before it, byte for byte
+    ri = next(i for i, f in enumerate(frames) if f[5] == "renderImage")
+    assert np.array_equal(read_ppm(frames[ri][1]), read_ppm(frames[ri - 1][1]))
+    # toggles as the settings printout reports them after the last key
+    last = lines[lines.index("------SETTINGS------", len(lines) - 14):]
+    assert last[1:7] == ["Ammbient ON", "Diffuse ON", "Specular ON", "Reflection OFF", "Shadow ON", "Refraction OFF"]
+    # 'd': the ray produceRay shot and the colour the session printed, against the oracle's trace
+    drays = [l.split()[1:] for l in lines if l.startswith("dray ")]
+    cols = [l for l in lines if l.startswith("Ray trace color = ")]
+    assert len(drays) == len(cols) == 2
+    p = O.make_params(w, h, pf=2, max_lvl=10, lights=[(0.0, 0.0, 4.0)] * 2, flags=_flags("111000"))   # shadows off then
+    for r, c in zip(drays, cols):
+        v = np.array([int(x, 16) for x in r], np.uint32).view(np.float32)
+        _, rgb = orc.debug_trace(p, v[:3], v[3:])
+        got = np.array([float(x) for x in c.split("(")[1].rstrip(")").split(",")], np.float32)
+        assert np.abs(got - rgb).max() <= 1e-6 + F32_TOL
+    assert "Ray trace history cleared" in lines
+
+
+@pytest.mark.gpu
+def test_dropin_literal_loop_uses_one_gpu_call_per_frame(dropin_bin, workdir, tmp_path, gpu_available):
+    """The unchanged 'r' loop at the reference's defaults (500 x 500, pf 3, max_lvl 10: 2.25M
+    performRayTracing calls): the drop-in answers the loop's sub-samples from one frame-wide GPU
+    trace, so the loop takes well under a second, and its frame equals renderImage()'s."""
+    path = scene_path("ref:dodgeColorTest.obj", workdir)
+    prefix = str(tmp_path / "g")
+    lines = _lines([dropin_bin, "keys", path, "500", "500", prefix, "T", "R", "P:300"])
+    fr = [l.split() for l in lines if l.startswith("frame ")]
+    assert float(fr[0][10]) < 5000.0   # ms: the whole literal loop
+    assert np.array_equal(read_ppm(fr[0][1]), read_ppm(fr[1][1]))
+    single = next(l.split() for l in lines if l.startswith("single "))
+    assert float(single[4]) > 0

@@ -170,8 +170,9 @@ def test_frame_device_equals_rectangle_render(size, pf, workdir, gpu_available):
                                                     ("syn:C4", (640, 360), 2, False)])
 def test_fused_pixel_writes_equal_frame_pass(spec, size, pf, want_f32, workdir, gpu_available):
     """RT_TUNE_FUSE_PIXELS: the chain launch writes each pixel when its samples' chains end (the
-    pf^2 sub-samples summed across adjacent lanes in k_frame's order; pf 3 does not divide a batch
-    and keeps the frame pass). Bytes, floats and ray counts equal the separate frame pass's, for
+    pf^2 sub-samples summed across adjacent lanes in k_frame's order; pf 3 packs 7 pixels into 63
+    lanes, and its batch order must not be taken from the unfused launch's 64-query batches).
+    Bytes, floats and ray counts equal the separate frame pass's, for
     the rectangle render, the whole-frame device render and the tile-major shard layout (whose
     pixels outside the frame are written black: ragged sizes leave partial tiles)."""
     import torch
