@@ -55,6 +55,11 @@ WORKLOADS = {
                     "the reference's regular AA grid), depth 3, 4 lights",
                scene="syn:C5", width=3840, height=2160, pf=2, max_lvl=3,
                lights=((0.0, 0.0, 4.0), (1.5, 1.5, 4.0), (-1.5, 1.5, 4.0), (0.0, -1.5, 4.0)), cpu_every=1024),
+    "ref_default": dict(desc="the reference's own defaults: dodgeColorTest.obj (16,311 tris) 500x500 window, pixelfactor 3 "
+                             "(9 sub-samples/pixel), max_lvl 10, light 0 = the camera (main.cpp:137-141, "
+                             "raytracing.cpp:23-29,72)",
+                        scene="ref:dodgeColorTest.obj", width=500, height=500, pf=3, max_lvl=10, lights=((0.0, 0.0, 4.0),),
+                        cpu_every=4, dropin=True),
     "c5s": dict(desc="C5 stochastic: synthetic 16x16 UV-sphere grid OBJ (1,015,810 tris) 3840x2160, 4 jittered "
                      "samples/pixel (RT_STOCHASTIC, seed 0x5EED: pf 2 strata, counter-hash jitter; an extension of "
                      "the reference's regular grid), depth 3, 4 lights",
@@ -100,6 +105,7 @@ def parse():
     ap.add_argument("--no-path-compare", action="store_true",
                     help="N=1: skip timing the shard path (tiles + un-permute) beside the frame path")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-dropin", action="store_true", help="ref_default: skip timing the drop-in's literal 'r' loop")
     ap.add_argument("--profile-steps", type=int, default=1, help="steps re-run with HIP events for the roofline")
     ap.add_argument("--ppm", default="", help="write the first frame to this PPM (rank 0)")
     ap.add_argument("--accel", choices=("bvh", "brute_force"), default="bvh")
@@ -315,20 +321,27 @@ def main():
                      "all_equal_one_gpu_frame": bool(all(torch.equal(frames[f], ref) for f in range(frames.shape[0]))),
                      "note": "ranks share one GPU; gloo host-staged gather: logic check, not a scaling number"}
 
-    # ---- a cold frame: no measured batch order yet (the first frame of a new view) ----
-    scene.tune("batch_order", 0)   # screen-order dispatch, exactly what a view's first launch does
-    cold = []
-    for i in range(0 if args.no_cold else 3):
+    # ---- a cold frame: the first frame of a new view (no measured batch order, no steal trial):
+    # the library orders it by its primary-walk estimate (RT_TUNE_COLD_ESTIMATE); for comparison
+    # the same frame dispatched in screen order ----
+    def cold_frame(i):
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
+        scene.tune("forget_order", 1)
         t0 = time.perf_counter()
         main_run.step(i)
         main_run.drain()
         torch.cuda.synchronize(dev)
-        cold.append(time.perf_counter() - t0)
-    scene.tune("batch_order", 1)
+        return time.perf_counter() - t0
+
+    cold = [cold_frame(i) for i in range(0 if args.no_cold else 3)]
+    scene.tune("cold_estimate", 0)
+    cold_screen = [cold_frame(i) for i in range(0 if args.no_cold else 3)]
+    scene.tune("cold_estimate", 1)
     cold_ms = sorted(cold)[1] * 1e3 if cold else None
+    cold_screen_ms = sorted(cold_screen)[1] * 1e3 if cold_screen else None
+    main_run.run(0, max(args.warmup, 3))   # re-learn the measured order before the other legs
 
     # ---- the same work through the other path: N=1 the shard path (tiles + un-permute, what
     # N>1 runs, minus the collective); N>1 strong scaling (one frame split over the ranks) ----
@@ -474,8 +487,10 @@ def main():
                 "rays_by_kind_per_step": {"primary": rays_by_kind[0], "secondary": rays_by_kind[1], "shadow": rays_by_kind[2]},
                 "frame_ms_per_gpu": round(elapsed / args.steps * 1e3, 3),
                 "first_frame_ms": round(cold_ms, 3) if cold_ms is not None else None,
-                "first_frame_what": "a frame with no measured batch order (screen-order dispatch, as a new view's "
-                                    "first launch), median of 3, synchronised",
+                "first_frame_what": "a new view's first frame (no measured batch order or steal trial: every order "
+                                    "forgotten first), ordered by the library's primary-walk estimate, median of 3, "
+                                    "synchronised",
+                "first_frame_screen_order_ms": round(cold_screen_ms, 3) if cold_screen_ms is not None else None,
                 "scene_load_s": round(t_load, 3), "scene_gen_s": round(t_gen, 3),
             },
             "roofline": {
@@ -520,6 +535,10 @@ def main():
         if args.ppm and frames is not None:
             R.write_ppm(args.ppm, frames[0].cpu().numpy())
 
+    # ---- the reference's own caller unchanged: main.cpp's 'r' loop over the source-level drop-in ----
+    if rank == 0 and world == 1 and wl.get("dropin") and not args.no_dropin:
+        result["dropin_loop"] = dropin_loop(obj, wl)
+
     # ---- CPU baseline + in-run parity on a bounded tile sample (rank 0, N=1 only) ----
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(obj, params, frames[0].cpu().numpy(), layout, args, wl)
@@ -562,6 +581,35 @@ def pmc_counters(kernel: str, need: str):
             if need in ks[n]:
                 return ks[n], os.path.relpath(f, HERE)
     return None, None
+
+
+def dropin_loop(obj, wl):
+    """main.cpp's 'r' key as written (one performRayTracing per sub-sample, then RGBValue and
+    Image::writeImage) compiled against include/raytracert_dropin.hpp: tests/cxx/dropin_main.cpp built
+    with g++ here, run as a child process on the same GPU. Times the literal loop (the drop-in answers
+    its sub-samples from one frame-wide trace), the one-call renderImage(), and single
+    performRayTracing calls on rays of no frame (the per-call round trip)."""
+    import subprocess
+    d = tempfile.mkdtemp(prefix="rt_dropin_")
+    exe = os.path.join(d, "dropin_main")
+    lib = os.path.join(HERE, "raytracert_amd")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-I" + os.path.join(HERE, "include"),
+                    os.path.join(HERE, "tests", "cxx", "dropin_main.cpp"), "-L" + lib, "-lrtamd", "-Wl,-rpath," + lib,
+                    "-o", exe], check=True)
+    # pf stays the reference's default 3 and max_lvl its 10 (the drop-in's globals); 'T' x2: the
+    # first frame includes the upload of the workspace
+    out = subprocess.run([exe, "keys", obj, str(wl["width"]), str(wl["height"]), os.path.join(d, "f"), "T", "T", "R",
+                          "P:2000"], check=True, capture_output=True, text=True, timeout=600).stdout.splitlines()
+    fr = [l.split() for l in out if l.startswith("frame ")]
+    single = next(l.split() for l in out if l.startswith("single "))
+    loop_ms = float(fr[1][10])
+    n = wl["width"] * wl["height"] * wl["pf"] ** 2
+    return {"what": "main.cpp:355-395 unchanged (performRayTracing per sub-sample) over the drop-in header, "
+                    f"{wl['width']}x{wl['height']} pf {wl['pf']} = {n} calls",
+            "loop_ms": loop_ms, "first_loop_ms": float(fr[0][10]), "render_image_ms": float(fr[2][7]),
+            "single_call_us": float(single[4]), "single_calls": int(single[1]),
+            "per_call_loop_estimate_s": round(float(single[4]) * n / 1e6, 1),
+            "frames_equal": open(fr[1][1], "rb").read() == open(fr[2][1], "rb").read()}
 
 
 def host_cpu():

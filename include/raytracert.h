@@ -282,6 +282,12 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
                                     batches (and at most 1/32 of them) run as two waves of 32 samples, the
                                     other 32 lanes of each starting as helpers (default 512; 0 off; only
                                     when 32 lanes hold whole pixels, i.e. pfx*pfy divides 32) */
+#define RT_TUNE_COLD_ESTIMATE 24 /* 1 (default): a fused launch over batches with no measured order (a new
+                                    view's first frame) is ordered by a pre-pass that walks one primary
+                                    ray per wave batch and scores the batch (walk cost, hit, shadows,
+                                    reflective or refractive material); 0: screen order */
+#define RT_TUNE_FORGET_ORDER 25  /* any value: drop every measured batch order and wave-steal trial, so the
+                                    next launch runs as a new view's first frame (benchmarks, tests) */
 #define RT_TUNE_STEAL_QUARTER 23 /* ... and before them this many of the longest run as four waves of 16
                                     samples each (48 helpers per wave; default 0; pfx*pfy divides 16) */
 #define RT_TUNE_TOP_NODES 13     /* four-wide nodes of the tree's top levels (breadth-first, the first

@@ -39,6 +39,7 @@ TUNE_XCD_SPLIT, TUNE_BVH_GRID, TUNE_BVH_WIDTH, TUNE_LDS_STACK, TUNE_PIPES, TUNE_
 TUNE_PIPE_BATCHES, TUNE_PIPE_PRIORITY, TUNE_WAVE_TRAVERSAL, TUNE_CHAIN_FROM = 6, 7, 8, 9
 TUNE_CHAIN_SPLIT, TUNE_TOP_NODES, TUNE_BATCH_ORDER, TUNE_ORDER_EVERY, TUNE_FUSE_PIXELS = 12, 13, 15, 17, 18
 TUNE_CHAIN_REFILL, TUNE_REFILL_GRID, TUNE_WAVE_STEAL = 19, 20, 21
+TUNE_COLD_ESTIMATE, TUNE_FORGET_ORDER = 24, 25
 TUNE_STEAL_HALF, TUNE_STEAL_QUARTER = 22, 23
 BVH_INFO_FIELDS = 7
 STOCHASTIC = 1 << 8

@@ -147,6 +147,10 @@ void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t strea
 constexpr int kOrderBuckets = 128;
 constexpr int kWaveBatch = 64;   // lanes per wave batch of the chain launch (one sample per lane)
 hipError_t launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream);
+// A cold launch's batch scores (no measured order yet): one primary walk per wave batch of a fused
+// launch (g, fuse_spp, capacity as launch_chain's), scored into score[batch] for launch_order_batches.
+void launch_estimate(const DevScene &s, const ShadeParams &p, const FrameGeom &g, int fuse_spp, int64_t capacity,
+                     uint32_t *score, hipStream_t stream);
 void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *dst, int32_t n,
                            int32_t *idx, float4 *I, hipStream_t stream);
 // calculateNormals on the device (face normal per triangle into normals[i].xyz)

@@ -341,6 +341,33 @@ def test_batch_order_from_previous_launch_keeps_results(mode, pf, size, workdir,
             assert np.array_equal(f32.view(np.uint32), fref.view(np.uint32))
 
 
+@pytest.mark.parametrize("spec,w,h,pf", [("syn:C4", 320, 180, 1), ("ref:dodgeColorTest.obj", 200, 150, 3),
+                                         ("syn:F4", 96, 54, 2), ("syn:F4", 17, 9, 1)])
+def test_cold_estimate_order_keeps_results(spec, w, h, pf, workdir, gpu_available):
+    """RT_TUNE_COLD_ESTIMATE: a new view's first launch is ordered by the primary-walk estimate
+    (k_estimate + the batch sort) instead of screen order; later launches by measured durations.
+    Every render after RT_TUNE_FORGET_ORDER (cold) and the warm ones after it are byte-identical
+    with identical ray counts to screen-order dispatch, with the frame and the shard entry."""
+    import torch
+    p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
+    with R.Scene.load(scene_path(spec, workdir), device=0) as sc:
+        sc.tune("batch_order", 0)
+        ref, reff, refc = sc.render(p, want_f32=True)
+        fb0 = torch.zeros(h * w * 3, dtype=torch.uint8, device="cuda:0")
+        sc.render_frame_device(p, 16, 16, fb0.data_ptr(), fb0.numel(), torch.cuda.current_stream().cuda_stream)
+        sc.tune("batch_order", 1)
+        for est in (1, 0, 1):
+            sc.tune("cold_estimate", est)
+            sc.tune("forget_order", 1)
+            for _ in range(3):
+                u8, f32, c = sc.render(p, want_f32=True)
+                assert [int(x) for x in c] == [int(x) for x in refc]
+                assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
+                fb = torch.full((h * w * 3,), 7, dtype=torch.uint8, device="cuda:0")
+                sc.render_frame_device(p, 16, 16, fb.data_ptr(), fb.numel(), torch.cuda.current_stream().cuda_stream)
+                assert torch.equal(fb, fb0)
+
+
 def test_multi_frame_shard_batch_reassembles(workdir, gpu_available):
     """Weak-scaling step shape: a batch of 3 frames of one view, ids g = f*T + t interleaved over 3
     ranks, one rt_render_tiles_device call per rank; every assembled frame equals the render."""
