@@ -385,6 +385,17 @@ def main():
         return st, work
 
     stats, (bvh_tests, bvh_visits, sh_bvh_tests, sh_bvh_visits) = profile(args.profile_steps, main_run)
+    # the wave batches of the latest (ordered) launch: the longest is the frame's critical path, the
+    # floor of any split of one frame over N GPUs (DESIGN.md §9's strong-scaling model)
+    batches = None
+    if world == 1 and args.accel == "bvh" and hasattr(R._capi.lib(), "rt_batch_durations"):   # (A/B builds may predate it)
+        main_run.render_once()
+        bd = scene.batch_durations()
+        if bd.size:
+            batches = {"n": int(bd.size), "max_us": round(float(bd.max()), 1), "p99_us": round(float(np.percentile(bd, 99)), 1),
+                       "median_us": round(float(np.median(bd)), 1), "sum_ms": round(float(bd.sum()) / 1e3, 2),
+                       "what": "per wave batch of one ordered chain launch: the wave's lifetime (s_memrealtime); max = the "
+                               "frame's critical path (one wave's chains), sum / launch time = mean resident waves"}
     chain_launches, chain_ms, chain_tests = stats[KERNEL_CHAIN]
     ch_launches, ch_ms, ch_tests = stats[KERNEL_CLOSEST_HIT]
     sh_launches, sh_ms, sh_tests = stats[KERNEL_SHADOW]
@@ -526,10 +537,14 @@ def main():
                 "chain": round(chain_ms / max(args.profile_steps, 1), 3),
             },
             "roofline_bruteforce": bf,
+            "batches": batches,
             "accel": {"mode": args.accel, "bvh": bvh_info},
             "cpu_baseline": None,
         }
         result.update(extra)
+        if world == 1 and batches:
+            result["strong_model"] = strong_model(elapsed / args.steps * 1e3, batches["max_us"] / 1e3,
+                                                  extra.get("shard_path", {}).get("ms_per_step"), WIDTH * HEIGHT * 3)
         if rehearsal is not None:
             result["rehearsal"] = rehearsal
         if args.ppm and frames is not None:
@@ -550,6 +565,28 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+def strong_model(t1_ms, crit_ms, shard_ms, frame_bytes, link_gbs=(50.0, 150.0), rccl_lat_ms=0.02, sync_ms=0.02):
+    """Per-frame time of ONE frame split over N GPUs (strong scaling), from one-GPU
+    measurements: each rank renders 1/N of the interleaved tiles, which cannot take less than the
+    frame's longest wave batch (its critical path, measured); then one RCCL gather to rank 0 over
+    xGMI (rank 0 receives frame_bytes / N from each of the N - 1 peers on its own link, at an
+    assumed 50-150 GB/s per link, plus a collective latency), the device un-permute (measured at
+    N = 1: the shard path minus the frame path) and a barrier."""
+    assemble_ms = max(0.0, (shard_ms or t1_ms) - t1_ms)
+    out = {"inputs": {"t1_ms": round(t1_ms, 4), "critical_path_ms": round(crit_ms, 4), "assemble_ms": round(assemble_ms, 4),
+                      "frame_bytes": frame_bytes, "link_gbs": list(link_gbs), "rccl_latency_ms": rccl_lat_ms,
+                      "sync_ms": sync_ms}}
+    for n in (2, 4, 8):
+        render = max(t1_ms / n, crit_ms)
+        res = {}
+        for bw in link_gbs:
+            gather = frame_bytes / n / (bw * 1e9) * 1e3 + rccl_lat_ms
+            t = render + gather + assemble_ms + sync_ms
+            res[f"{int(bw)}GBs"] = {"ms_per_frame": round(t, 4), "speedup": round(t1_ms / t, 2)}
+        out[f"n{n}"] = {"render_ms": round(render, 4), "bound": "critical path" if crit_ms >= t1_ms / n else "work / N", **res}
+    return out
 
 
 def pmc_traffic(kernel: str):

@@ -290,8 +290,9 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
                                     next launch runs as a new view's first frame (benchmarks, tests) */
 #define RT_TUNE_STEAL_QUARTER 23 /* ... and before them this many of the longest run as four waves of 16
                                     samples each (48 helpers per wave; default 0; pfx*pfy divides 16) */
-#define RT_TUNE_TOP_NODES 13     /* four-wide nodes of the tree's top levels (breadth-first, the first
-                                    ones in the node array) each block reads from an LDS copy (0-85) */
+#define RT_TUNE_TOP_NODES 13     /* retired in r03 (0-85 accepted, no effect): an LDS copy of the four-wide
+                                    tree's top levels; with float node rows loaded from global memory it
+                                    measured slower (flat loads, 64-bit addresses) */
 #define RT_TUNE_CHAIN_SPLIT 12   /* query distribution of the chain launch: as RT_TUNE_XCD_SPLIT, or 3: 64-query
                                     chunks dealt round-robin to the XCDs and taken dynamically within
                                     each */
@@ -336,6 +337,11 @@ int rt_work_detail(rt_scene *scene, int32_t kind, uint64_t out[RT_WORK_FIELDS]);
  * and stamp builds were retired with the variants they measured); 0 in production builds.
  * Reads count words from offset (offset + count <= 131072); synchronises the device. */
 int rt_diag_read(rt_scene *scene, int64_t offset, int64_t count, uint64_t *out);
+/* Per wave batch of the scene's latest chain launch (pipeline 0): the wave's duration in 100 MHz
+ * ticks (s_memrealtime), in batch order (screen order of the batches, not dispatch order). *n_out =
+ * the number of batches; up to capacity are copied. Synchronises the device. The longest batch is the
+ * launch's critical path (what an N-GPU split of the frame cannot go below). */
+int rt_batch_durations(rt_scene *scene, uint32_t *ticks, int64_t capacity, int64_t *n_out);
 /* The render workspace of one pipeline for `cap` samples, `steps` = max_lvl + 1 chain steps and
  * `lights` lights, as the library carves it (no allocation, no device): total bytes and, per array
  * in carving order, (offset, bytes): q_org[0], q_dst[0], q_org[1], q_dst[1], hit_idx, hit_I, sq_org,

@@ -112,6 +112,7 @@ _SIGNATURES = {
     "rt_work_detail": ([_VP, C.c_int32, _VP], C.c_int),
     "rt_diag_read": ([_VP, C.c_int64, C.c_int64, _VP], C.c_int),
     "rt_workspace_layout": ([C.c_int64, C.c_int32, C.c_int32, C.POINTER(C.c_uint64), _VP], C.c_int),
+    "rt_batch_durations": ([_VP, _VP, C.c_int64, C.POINTER(C.c_int64)], C.c_int),
     "rt_scene_bvh_digest": ([_VP, C.POINTER(C.c_uint64)], C.c_int),
     "rt_scene_bvh_validate": ([_VP], C.c_int),
     "rt_bvh_acceptance_box": ([_VP, _VP, _VP], C.c_int),
@@ -152,7 +153,10 @@ def lib() -> C.CDLL:
         except ImportError:
             pass
         L = C.CDLL(LIB_PATH)
+        ab = "RTAMD_LIB" in os.environ   # an A/B build of an older revision may lack newer entries
         for name, (args, res) in _SIGNATURES.items():
+            if ab and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res

@@ -278,6 +278,16 @@ class Scene:
              "forget_order": _capi.TUNE_FORGET_ORDER}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
 
+    def batch_durations(self) -> np.ndarray:
+        """Per wave batch of the latest chain launch: the wave's duration in microseconds
+        (rt_batch_durations; 100 MHz ticks). Its maximum is the launch's critical path."""
+        n = C.c_int64()
+        check(lib().rt_batch_durations(self._h, None, 0, C.byref(n)))
+        out = np.zeros(n.value, np.uint32)
+        if n.value:
+            check(lib().rt_batch_durations(self._h, out.ctypes.data, n.value, C.byref(n)))
+        return out.astype(np.float64) * 0.01
+
     def bvh_digest(self) -> int:
         """FNV-1a digest of the device BVH arrays (identical trees <=> equal digests)."""
         d = C.c_uint64()

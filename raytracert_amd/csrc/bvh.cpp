@@ -311,11 +311,24 @@ bool make_node4(const Box *boxes, const int32_t *refs, int nc, Bvh4Node &g) {
     return true;
 }
 
+Bvh4F make_node4f(const Box *boxes, const int32_t *refs, int nc) {
+    Bvh4F g{};
+    for (int c = 0; c < 4; ++c) {
+        g.child[c] = c < nc ? refs[c] : kBvhEmpty;
+        for (int k = 0; k < 3; ++k) {
+            g.lo[k][c] = c < nc ? boxes[c].lo[k] : INFINITY;   // empty: inverted, rejected by any slab test
+            g.hi[k][c] = c < nc ? boxes[c].hi[k] : -INFINITY;
+        }
+    }
+    return g;
+}
+
 // Collapse the binary build tree into four-wide nodes: repeatedly open the largest-area inner
 // child until a node has four children (the usual SAH-driven collapse), depth-first order.
 struct Collapser {
     const Builder &b;
     std::vector<Bvh4Node> &out;
+    std::vector<Bvh4F> &outf;
     int depth = 0;
     bool ok = true;
     int run(int n, int level) {
@@ -334,6 +347,7 @@ struct Collapser {
         }
         const int id = static_cast<int>(out.size());
         out.emplace_back();
+        outf.emplace_back();
         depth = std::max(depth, level);
         Box boxes[4];
         int32_t refs[4];
@@ -346,14 +360,15 @@ struct Collapser {
         Bvh4Node g;
         ok = ok && make_node4(boxes, refs, nc, g);
         out[id] = g;
+        outf[id] = make_node4f(boxes, refs, nc);
         return id;
     }
 };
 
 // Renumber the four-wide nodes so the top `levels` levels come first in breadth-first order
 // (the root stays 0); deeper nodes keep their depth-first order. Kernels keep a prefix of the
-// node array in LDS (DevScene::top_nodes), so the prefix must be the levels every query visits.
-void top_levels_first(std::vector<Bvh4Node> &nodes, int levels) {
+// node array (the levels every query visits) together, at the start of the array.
+void top_levels_first(std::vector<Bvh4Node> &nodes, std::vector<Bvh4F> &nodesf, int levels) {
     const size_t n = nodes.size();
     if (n <= 1) return;
     std::vector<int> order{0}, lvl{0};
@@ -375,12 +390,15 @@ void top_levels_first(std::vector<Bvh4Node> &nodes, int levels) {
     std::vector<int32_t> id(n);
     for (size_t k = 0; k < n; ++k) id[order[k]] = static_cast<int32_t>(k);
     std::vector<Bvh4Node> out(n);
+    std::vector<Bvh4F> outf(n);
     for (size_t k = 0; k < n; ++k) {
         out[k] = nodes[order[k]];
+        outf[k] = nodesf[order[k]];
         for (int c = 0; c < 4; ++c)
-            if (out[k].child[c] >= 0) out[k].child[c] = id[out[k].child[c]];
+            if (out[k].child[c] >= 0) outf[k].child[c] = out[k].child[c] = id[out[k].child[c]];
     }
     nodes.swap(out);
+    nodesf.swap(outf);
 }
 
 }  // namespace
@@ -457,6 +475,7 @@ int build_bvh(const HostScene &s, const std::vector<TriRec> &recs, HostBvh &out)
         out.depth = 1;
         out.nodes4.emplace_back();
         make_node4(nullptr, nullptr, 0, out.nodes4[0]);
+        out.nodes4f.push_back(make_node4f(nullptr, nullptr, 0));
         out.depth4 = 1;
         return RT_OK;
     }
@@ -490,13 +509,14 @@ int build_bvh(const HostScene &s, const std::vector<TriRec> &recs, HostBvh &out)
         const int32_t r = leaf_ref(b.nodes[0]);
         out.nodes4.emplace_back();
         if (!make_node4(&b.nodes[0].box, &r, 1, out.nodes4[0])) return RT_E_ARG;
+        out.nodes4f.push_back(make_node4f(&b.nodes[0].box, &r, 1));
         out.depth4 = 1;
     } else {
-        Collapser c{b, out.nodes4};
+        Collapser c{b, out.nodes4, out.nodes4f};
         c.run(0, 1);
         if (!c.ok) return RT_E_ARG;   // a box no 8-bit grid can bound (coordinates near FLT_MAX)
         out.depth4 = c.depth;
-        top_levels_first(out.nodes4, kTopLevels4);
+        top_levels_first(out.nodes4, out.nodes4f, kTopLevels4);
     }
     if (b.nodes[0].left < 0) {   // the whole tree is one leaf: wrap it in a root with an empty sibling
         BvhNode root{};
@@ -523,6 +543,53 @@ int build_bvh(const HostScene &s, const std::vector<TriRec> &recs, HostBvh &out)
 }
 
 namespace {
+// The float four-wide nodes (what the kernels read): the same topology as the quantised ones, and
+// every child box contains everything below it (its child boxes, its leaf triangles' padded
+// acceptance boxes); empty slots are inverted boxes.
+int validate_bvh4f(const HostScene &s, const std::vector<TriRec> &recs, const HostBvh &h, std::string &err) {
+    if (h.nodes4f.size() != h.nodes4.size()) { err = "4-wide float: node count differs"; return RT_E_PARSE; }
+    struct Item { int32_t ref; float lo[3], hi[3]; };
+    std::vector<Item> st{Item{0, {-INFINITY, -INFINITY, -INFINITY}, {INFINITY, INFINITY, INFINITY}}};
+    while (!st.empty()) {
+        const Item it = st.back();
+        st.pop_back();
+        if (it.ref == kBvhEmpty) continue;
+        if (static_cast<uint32_t>(it.ref) & kBvhLeafBit) {
+            const uint32_t u = static_cast<uint32_t>(it.ref);
+            const uint32_t cnt = (u >> kBvhCountShift) & kBvhCountMask, first = u & ((1u << kBvhCountShift) - 1);
+            for (uint32_t i = first; i < first + cnt; ++i) {
+                const uint32_t t = h.leaf_tris[i];
+                float lo[3], hi[3];
+                bool never;
+                acceptance_box(recs[t], &s.verts[3 * s.tris[3 * t]], &s.verts[3 * s.tris[3 * t + 1]],
+                               &s.verts[3 * s.tris[3 * t + 2]], lo, hi, &never);
+                for (int k = 0; k < 3; ++k)
+                    if (lo[k] < it.lo[k] || hi[k] > it.hi[k]) { err = "4-wide float: triangle box outside its leaf box"; return RT_E_PARSE; }
+            }
+            continue;
+        }
+        if (it.ref < 0 || static_cast<size_t>(it.ref) >= h.nodes4f.size()) { err = "4-wide float: bad node ref"; return RT_E_PARSE; }
+        const Bvh4F &g = h.nodes4f[it.ref];
+        const Bvh4Node &q = h.nodes4[it.ref];
+        for (int c = 0; c < 4; ++c) {
+            if (g.child[c] != q.child[c]) { err = "4-wide float: child refs differ from the quantised node"; return RT_E_PARSE; }
+            Item ch{g.child[c], {}, {}};
+            for (int k = 0; k < 3; ++k) {
+                ch.lo[k] = g.lo[k][c];
+                ch.hi[k] = g.hi[k][c];
+                if (c >= q.n_children) {
+                    if (!(ch.lo[k] == INFINITY && ch.hi[k] == -INFINITY)) { err = "4-wide float: empty slot not inverted"; return RT_E_PARSE; }
+                } else if (ch.lo[k] < it.lo[k] || ch.hi[k] > it.hi[k]) {
+                    err = "4-wide float: child box outside its parent's";
+                    return RT_E_PARSE;
+                }
+            }
+            if (c < q.n_children) st.push_back(ch);
+        }
+    }
+    return RT_OK;
+}
+
 // The four-wide tree: decoded child boxes contain everything below them (nested boxes and padded
 // triangle boxes), every tree triangle in exactly one leaf, every node reached once, the stack
 // bound 3 * depth4 holds.
@@ -642,7 +709,8 @@ int validate_bvh(const HostScene &s, const std::vector<TriRec> &recs, const Host
     }
     if (inner_seen != h.nodes.size()) { err = "unreachable nodes"; return RT_E_PARSE; }
     if (never != h.n_never) { err = "degenerate count mismatch"; return RT_E_PARSE; }
-    return validate_bvh4(s, recs, h, err);
+    const int rc = validate_bvh4(s, recs, h, err);
+    return rc ? rc : validate_bvh4f(s, recs, h, err);
 }
 
 uint64_t bvh_digest(const HostBvh &h) {
@@ -653,6 +721,7 @@ uint64_t bvh_digest(const HostBvh &h) {
     };
     mix(h.nodes.data(), h.nodes.size() * sizeof(BvhNode));
     mix(h.nodes4.data(), h.nodes4.size() * sizeof(Bvh4Node));
+    mix(h.nodes4f.data(), h.nodes4f.size() * sizeof(Bvh4F));
     mix(h.leaf_tris.data(), h.leaf_tris.size() * sizeof(uint32_t));
     mix(h.always.data(), h.always.size() * sizeof(uint32_t));
     return x;

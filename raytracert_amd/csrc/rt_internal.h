@@ -90,9 +90,23 @@ struct alignas(16) Bvh4Node {
 };
 static_assert(sizeof(Bvh4Node) == 64, "Bvh4Node must be 64 bytes");
 
+// The same four-wide node with float child boxes, the layout the kernels traverse: per axis k the
+// four children's lower bounds (lo[k][c]) and upper bounds (hi[k][c]) as float4 rows, so a lane
+// loads the near and far rows its ray direction needs by address (row k or 3 + k) and each slab
+// plane of each child costs one FMA; the boxes are the children's padded acceptance-box unions
+// themselves (no quantisation). Empty slots hold an inverted box (lo = +inf, hi = -inf).
+struct alignas(16) Bvh4F {
+    float lo[3][4];
+    float hi[3][4];
+    int32_t child[4];     // inner node index, leaf ref (kBvhLeafBit | count << 21 | first) or kBvhEmpty
+    int32_t pad[4];
+};
+static_assert(sizeof(Bvh4F) == 128, "Bvh4F must be 128 bytes");
+
 struct HostBvh {
     std::vector<BvhNode> nodes;       // nodes[0] is the root
     std::vector<Bvh4Node> nodes4;     // the same tree collapsed to four-wide nodes; nodes4[0] is the root
+    std::vector<Bvh4F> nodes4f;       // nodes4 with float child boxes (same topology and order): what kernels read
     int depth4 = 0;                   // inner levels of the four-wide tree
     std::vector<uint32_t> leaf_tris;  // original triangle index of each leaf slot
     std::vector<uint32_t> always;     // ill-conditioned triangles every query tests

@@ -73,7 +73,7 @@ struct DevScene {
     int32_t use_bvh, n_always;
     float scene_m1;
     int32_t bvh_depth;              // traversal stack entries needed (tree depth)
-    const Bvh4Node *nodes4;         // the four-wide tree (bvh_width == 4)
+    const Bvh4F *nodes4f;           // the four-wide tree (bvh_width == 4), float child boxes
     int32_t bvh_width;              // 2 or 4 (RT_TUNE_BVH_WIDTH)
     int32_t lds_stack;              // stack entries per lane held in LDS (<= entries needed)
     int32_t *stack_ovf;             // deeper entries: [entry - lds_stack][grid lane], grid <= bvh_grid
@@ -81,7 +81,6 @@ struct DevScene {
     int32_t bvh_grid;               // RT_TUNE_BVH_GRID
     unsigned long long *work;       // BVH kernels' work counters: [0, kWorkFields) closest-hit, then shadow
     int32_t chain_split;            // RT_TUNE_CHAIN_SPLIT: query distribution of k_chain (as xcd_split)
-    int32_t top_nodes;              // RT_TUNE_TOP_NODES: four-wide nodes [0, top_nodes) read from an LDS copy
     int32_t wave_steal;             // RT_TUNE_WAVE_STEAL: 0 off, 1 on, 2 when the chain launch is <= 2 wave rounds
     int32_t resident_grid;          // chain-kernel blocks resident on the device at once (CUs x blocks per CU)
     int32_t steal_half;             // RT_TUNE_STEAL_HALF: half-wave batches of the ordered stealing launch
@@ -156,9 +155,10 @@ void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *d
 // calculateNormals on the device (face normal per triangle into normals[i].xyz)
 void launch_face_normals(const float *xyz, const uint32_t *tri_v, int32_t nt, float4 *normals, hipStream_t stream);
 // Un-permute gathered tile shards ([nranks][slots][th][tw][3], tile g of the frames x T tiles in
-// rank g % nranks, slot g / nranks) into frames x height x width x 3 bytes.
+// rank g % nranks, slot g / nranks) into frames x height x width x 3 bytes; with slot0 / nslots, a
+// gather chunk holding slots [slot0, slot0 + nslots) of every rank ([nranks][nslots][th][tw][3]).
 void launch_assemble_tiles(const uint8_t *gathered, int32_t width, int32_t height, int32_t tw, int32_t th, int32_t frames,
-                           int32_t nranks, uint8_t *out, hipStream_t stream);
+                           int32_t nranks, uint8_t *out, hipStream_t stream, int64_t slot0 = 0, int64_t nslots = -1);
 // rayIntersectTriangle for n (ray, triangle) pairs: R = n x (origin, dest), T = n x 3 vertices
 void launch_ray_triangle_pairs(const float *R, const float *T, int32_t n, uint8_t *hit, float *I, hipStream_t stream);
 

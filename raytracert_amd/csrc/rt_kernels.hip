@@ -208,8 +208,6 @@ struct LaneStack {
     int32_t *lds;       // [entry][width lanes]
     int32_t *ovf;
     int cap, stride, gl, width;
-    const uint4 *top;   // LDS copy of the four-wide node array's first ntop nodes (the top levels)
-    int ntop;
     __device__ __forceinline__ void push(int &sp, int32_t v) const {
         if (sp < cap) lds[sp * width + static_cast<int>(threadIdx.x)] = v;
         else ovf[static_cast<size_t>(sp - cap) * stride + gl] = v;
@@ -230,8 +228,7 @@ struct LaneStack {
     }
 };
 
-// Dynamic LDS of the per-lane BVH kernels: [lds_stack entries][128 lanes] of stack, then the top
-// nodes. Every thread of the block must call this before its first query (barrier).
+// Dynamic LDS of the per-lane BVH kernels: [lds_stack entries][block lanes] of stack.
 template <int B = kBvhBlock>
 __device__ __forceinline__ LaneStack lane_stack(const DevScene &sc, int32_t *lds) {
     LaneStack st;
@@ -241,30 +238,28 @@ __device__ __forceinline__ LaneStack lane_stack(const DevScene &sc, int32_t *lds
     st.cap = sc.lds_stack;
     st.stride = static_cast<int>(gridDim.x) * B;
     st.gl = static_cast<int>(blockIdx.x) * B + static_cast<int>(threadIdx.x);
-    uint4 *top = reinterpret_cast<uint4 *>(lds + static_cast<size_t>(max(sc.lds_stack, 1)) * B);
-    st.top = top;
-    st.ntop = sc.top_nodes;
-    if (sc.top_nodes > 0) {
-        const uint4 *__restrict__ src = reinterpret_cast<const uint4 *>(sc.nodes4);
-        for (int i = threadIdx.x; i < 4 * sc.top_nodes; i += blockDim.x) top[i] = src[i];
-        __syncthreads();
-    }
     return st;
 }
 
-// A four-wide node's 64 bytes: from the LDS copy for the top levels, else from the node array.
-#ifndef RT_TOP_LDS
-#define RT_TOP_LDS 1   // 0 (A/B): no LDS node cache, so node loads are global loads, not flat ones
-#endif
-__device__ __forceinline__ void load_node4(const LaneStack &stack, const Bvh4Node *__restrict__ nodes4, int32_t ref,
-                                           uint4 &a, uint4 &b, uint4 &c, uint4 &d) {
-    if (RT_TOP_LDS && ref < stack.ntop) {
-        const uint4 *p = stack.top + 4 * ref;
-        a = p[0]; b = p[1]; c = p[2]; d = p[3];
-    } else {
-        const uint4 *p = reinterpret_cast<const uint4 *>(nodes4 + ref);
-        a = p[0]; b = p[1]; c = p[2]; d = p[3];
+// A four-wide node's rows for this ray (Bvh4F): the near and far bound rows of each axis (the
+// lower bounds are the near plane when the ray's direction component is positive, the upper bounds
+// when it is negative; Ray4::rows holds the byte offsets) and the child refs, as global loads from
+// the node array's base plus a 32-bit per-lane offset, so the first row's FMAs start while the
+// others are in flight. (An LDS copy of the top levels, read through flat loads with 64-bit row
+// addresses, measured 2% slower on C4 and 18% on C5: profiles/r03_ab_float_nodes.txt.)
+struct Node4Rows { float4 n[3], f[3]; int4 ref; };
+__device__ __forceinline__ Node4Rows load_node4(const Bvh4F *__restrict__ nodes4, int32_t ref, const uint32_t (&rows)[6]) {
+    Node4Rows r;
+    // global loads from the node array's base (wave-uniform) plus a 32-bit per-lane byte offset
+    const char *__restrict__ base = reinterpret_cast<const char *>(nodes4);
+    const uint32_t o = static_cast<uint32_t>(ref) * static_cast<uint32_t>(sizeof(Bvh4F));
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        r.n[k] = *reinterpret_cast<const float4 *>(base + (o + rows[k]));
+        r.f[k] = *reinterpret_cast<const float4 *>(base + (o + rows[3 + k]));
     }
+    r.ref = *reinterpret_cast<const int4 *>(base + (o + static_cast<uint32_t>(offsetof(Bvh4F, child))));
+    return r;
 }
 
 __device__ __forceinline__ bool box_hit(const RayBox &R, float lx, float ly, float lz, float hx, float hy, float hz,
@@ -385,13 +380,9 @@ __device__ __forceinline__ void bvh_query(const DevScene &sc, V3 o, V3 dir, bool
     }
 }
 
-// Four-wide traversal over the quantised nodes (bvh.cpp, Bvh4Node). Same cull and leaf logic as
-// bvh_query; the hit children are sorted by entry distance, the nearest is visited next and the
-// others are pushed farthest first.
-__device__ __forceinline__ float q_decode(float base, float scale, uint32_t word, int c) {
-    return fmaf(static_cast<float>((word >> (8 * c)) & 0xFFu), scale, base);   // q * scale is exact
-}
-
+// Four-wide traversal (bvh.cpp, Bvh4F): the same cull and leaf logic as bvh_query; the hit
+// children are sorted by entry distance, the nearest is visited next and the others are pushed
+// farthest first.
 __device__ __forceinline__ void cswap(float &ta, int32_t &ra, float &tb, int32_t &rb) {
     const bool sw = tb < ta;
     const float t = sw ? tb : ta;
@@ -414,16 +405,16 @@ __device__ __forceinline__ void cswap(float &ta, int32_t &ra, float &tb, int32_t
 constexpr int32_t kDoneRef = kBvhEmpty;   // "no ref": a count-0 leaf is never a wanted child
 
 // Per-ray traversal constants. A child's slab plane is
-//   t = fma(q, 2^e * inv, fma(origin, inv, (-/+pad - o) * inv))
-// instead of (origin + q 2^e - o -/+ pad) * inv: the same value up to a few ulps of
-// (|o| + pad) * |inv| and of |t|, inside the pad (64 ulps of |o| + the scene's extent) and the
+//   t = fma(b, inv, (-/+pad - o) * inv)
+// for the plane's float bound b (Bvh4F), instead of (b -/+ pad - o) * inv: the same value up to a few
+// ulps of (|o| + pad) * |inv| and of |t|, inside the pad (64 ulps of |o| + the scene's extent) and the
 // 1e-5 relative slack of the te <= tx test.
 struct Ray4 {
     V3 o, inv;
     float tcull;
     float bnx, bny, bnz, bfx, bfy, bfz;   // (+/-pad - o) * inv per axis, near and far plane
     float inv_dlen;                       // an upper bound of 1.00001 / |dir|
-    bool nx, ny, nz;
+    uint32_t rows[6];                     // byte offsets in a Bvh4F of the near rows (x, y, z), then the far rows
 };
 
 // tcull for the current best: no child whose entry parameter exceeds it can hold a hit at
@@ -436,28 +427,19 @@ __device__ __forceinline__ float cull_param(const Ray4 &R, float best, float pad
 // One node visit: the wanted children by entry distance, the far ones pushed; returns the next ref
 // (the nearest wanted child, else the stack top, else kDoneRef). Entries [base, sp) are this walk's.
 template <bool kAnyHit>
-__device__ __forceinline__ int32_t node4_next(const Ray4 &R, uint4 a, uint4 b, uint4 c, uint4 d, const LaneStack &stack,
-                                              int &sp, int base = 0) {
+__device__ __forceinline__ int32_t node4_next(const Ray4 &R, const Node4Rows &nd, const LaneStack &stack, int &sp,
+                                              int base = 0) {
     const V3 inv = R.inv;
-    // 2^e * inv is exact (or the same overflow); v_ldexp_f32 takes the int8 exponent
-    const float kx = __builtin_amdgcn_ldexpf(inv.x, static_cast<int>(static_cast<int8_t>(a.w)));
-    const float ky = __builtin_amdgcn_ldexpf(inv.y, static_cast<int>(static_cast<int8_t>(a.w >> 8)));
-    const float kz = __builtin_amdgcn_ldexpf(inv.z, static_cast<int>(static_cast<int8_t>(a.w >> 16)));
-    const float ox = __uint_as_float(a.x), oy = __uint_as_float(a.y), oz = __uint_as_float(a.z);
-    const float cnx = fmaf(ox, inv.x, R.bnx), cfx = fmaf(ox, inv.x, R.bfx);
-    const float cny = fmaf(oy, inv.y, R.bny), cfy = fmaf(oy, inv.y, R.bfy);
-    const float cnz = fmaf(oz, inv.z, R.bnz), cfz = fmaf(oz, inv.z, R.bfz);
-    const uint32_t wnx = R.nx ? b.w : b.x, wfx = R.nx ? b.x : b.w;   // qlo / qhi words per axis
-    const uint32_t wny = R.ny ? c.x : b.y, wfy = R.ny ? b.y : c.x;
-    const uint32_t wnz = R.nz ? c.y : b.z, wfz = R.nz ? b.z : c.y;
-    int32_t rc[4] = {static_cast<int32_t>(c.z), static_cast<int32_t>(c.w), static_cast<int32_t>(d.x),
-                     static_cast<int32_t>(d.y)};
+    const float nx[4] = {nd.n[0].x, nd.n[0].y, nd.n[0].z, nd.n[0].w}, fx[4] = {nd.f[0].x, nd.f[0].y, nd.f[0].z, nd.f[0].w};
+    const float ny[4] = {nd.n[1].x, nd.n[1].y, nd.n[1].z, nd.n[1].w}, fy[4] = {nd.f[1].x, nd.f[1].y, nd.f[1].z, nd.f[1].w};
+    const float nz[4] = {nd.n[2].x, nd.n[2].y, nd.n[2].z, nd.n[2].w}, fz[4] = {nd.f[2].x, nd.f[2].y, nd.f[2].z, nd.f[2].w};
+    int32_t rc[4] = {nd.ref.x, nd.ref.y, nd.ref.z, nd.ref.w};
     float tc[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const float tnx = q_decode(cnx, kx, wnx, k), tfx = q_decode(cfx, kx, wfx, k);
-        const float tny = q_decode(cny, ky, wny, k), tfy = q_decode(cfy, ky, wfy, k);
-        const float tnz = q_decode(cnz, kz, wnz, k), tfz = q_decode(cfz, kz, wfz, k);
+        const float tnx = fmaf(nx[k], inv.x, R.bnx), tfx = fmaf(fx[k], inv.x, R.bfx);
+        const float tny = fmaf(ny[k], inv.y, R.bny), tfy = fmaf(fy[k], inv.y, R.bfy);
+        const float tnz = fmaf(nz[k], inv.z, R.bnz), tfz = fmaf(fz[k], inv.z, R.bfz);
         const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
         const float tx = fminf(fminf(tfx, tfy), tfz);
         bool h = te <= tx * 1.00001f;
@@ -519,8 +501,9 @@ __device__ __forceinline__ int32_t node4_next(const Ray4 &R, uint4 a, uint4 b, u
 // 1-ulp change of one axis' scale moves its slab parameters by 2^-23 relative, inside the 1e-5
 // slack of the te <= tx test and the tcull bound. inv is clamped to |inv| <= 2^100 (dir
 // components of 0 or below 2^-100): with the scene below 1e6 in magnitude (dev_view falls back to
-// the binary tree otherwise) no slab distance can be NaN, and a clamped axis only narrows a slab
-// where no hit can exist (|n.dir| >= 1e-5 needs |dir| >= 2.5e-18 there).
+// the binary tree otherwise) no slab distance can be NaN (an empty slot's infinite bound gives
+// +/-inf, rejected), and a clamped axis only narrows a slab where no hit can exist (|n.dir| >= 1e-5
+// needs |dir| >= 2.5e-18 there).
 __device__ __forceinline__ void ray4_setup(const DevScene &sc, V3 o, V3 dir, Ray4 &R, float &pad) {
     V3 inv = mk(__builtin_amdgcn_rcpf(dir.x), __builtin_amdgcn_rcpf(dir.y), __builtin_amdgcn_rcpf(dir.z));
     constexpr float kInvMax = 0x1p100f;
@@ -532,10 +515,13 @@ __device__ __forceinline__ void ray4_setup(const DevScene &sc, V3 o, V3 dir, Ray
     R.inv_dlen = __builtin_amdgcn_rsqf(dot(dir, dir)) * 1.00011f;
     R.o = o;
     R.inv = inv;
-    R.nx = inv.x < 0; R.ny = inv.y < 0; R.nz = inv.z < 0;
-    const float pnx = R.nx ? pad : -pad, pny = R.ny ? pad : -pad, pnz = R.nz ? pad : -pad;   // near = lo - pad / hi + pad
+    const bool nx = inv.x < 0, ny = inv.y < 0, nz = inv.z < 0;
+    const float pnx = nx ? pad : -pad, pny = ny ? pad : -pad, pnz = nz ? pad : -pad;   // near = lo - pad / hi + pad
     R.bnx = (pnx - o.x) * inv.x; R.bny = (pny - o.y) * inv.y; R.bnz = (pnz - o.z) * inv.z;
     R.bfx = (-pnx - o.x) * inv.x; R.bfy = (-pny - o.y) * inv.y; R.bfz = (-pnz - o.z) * inv.z;
+    constexpr uint32_t kLo = offsetof(Bvh4F, lo), kHi = offsetof(Bvh4F, hi), kRow = sizeof(float4);
+    R.rows[0] = (nx ? kHi : kLo); R.rows[1] = (ny ? kHi : kLo) + kRow; R.rows[2] = (nz ? kHi : kLo) + 2 * kRow;
+    R.rows[3] = (nx ? kLo : kHi); R.rows[4] = (ny ? kLo : kHi) + kRow; R.rows[5] = (nz ? kLo : kHi) + 2 * kRow;
     R.tcull = INFINITY;
 }
 
@@ -555,9 +541,7 @@ __device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, 
     while (true) {
         while (node >= 0) {
             ++visits;
-            uint4 a, b, c, d;
-            load_node4(stack, sc.nodes4, node, a, b, c, d);
-            node = node4_next<kAnyHit>(R, a, b, c, d, stack, sp);
+            node = node4_next<kAnyHit>(R, load_node4(sc.nodes4f, node, R.rows), stack, sp);
             if (node < 0 && node != kDoneRef && leaf == kDoneRef) {   // postpone it, keep walking
                 leaf = node;
                 node = sp ? stack.pop(sp) : kDoneRef;
@@ -707,9 +691,7 @@ __device__ __forceinline__ void bvh4_query_steal(const DevScene &sc, V3 o, V3 di
         }
         while (node >= 0) {
             ++visits;
-            uint4 a, b, c, d;
-            load_node4(stack, sc.nodes4, node, a, b, c, d);
-            node = node4_next<kAnyHit>(R, a, b, c, d, stack, sp, base);
+            node = node4_next<kAnyHit>(R, load_node4(sc.nodes4f, node, R.rows), stack, sp, base);
             if (node < 0 && node != kDoneRef && leaf == kDoneRef) {   // postpone it, keep walking
                 leaf = node;
                 node = sp > base ? stack.pop(sp) : kDoneRef;
@@ -1805,20 +1787,22 @@ __global__ __launch_bounds__(kBlock) void k_ray_triangle_pairs(const float *__re
     I[3 * i] = out.x; I[3 * i + 1] = out.y; I[3 * i + 2] = out.z;
 }
 
-// Un-permute of gathered tile shards (multi-GPU frame): gathered = [rank][slot]
-// tiles of tw x th x 3 bytes, global tile id g = f * T + t held by rank g % N in slot g / N. One
-// thread per row of a gathered tile: it copies the row's (clipped) tw x 3 bytes to the frame, in
-// 16-B pieces when both ends are 16-B aligned (tw = 16 at 1920 wide: always). Index math per tile
-// row, not per byte (the per-pixel form's 64-bit divisions cost ~20 us per C4 frame).
+// Un-permute of gathered tile shards (multi-GPU frame): gathered = [rank][nslots]
+// tiles of tw x th x 3 bytes, the slots slot0 .. slot0 + nslots - 1 of every rank's shard (one gather
+// chunk; the whole shard when slot0 = 0, nslots = slots); global tile id g = f * T + t is held by rank
+// g % N in slot g / N. One thread per row of a gathered tile: it copies the row's (clipped) tw x 3
+// bytes to the frame, in 16-B pieces when both ends are 16-B aligned (tw = 16 at 1920 wide: always).
+// Index math per tile row, not per byte (the per-pixel form's 64-bit divisions cost ~20 us per C4
+// frame).
 __global__ __launch_bounds__(kBlock) void k_assemble_tiles(const uint8_t *__restrict__ gathered, int32_t width,
                                                            int32_t height, int32_t tw, int32_t th, int32_t tiles_x,
-                                                           int32_t tiles_total, int32_t nranks, int64_t slots,
-                                                           int32_t frames, uint8_t *__restrict__ out) {
+                                                           int32_t tiles_total, int32_t nranks, int64_t slot0,
+                                                           int64_t nslots, int32_t frames, uint8_t *__restrict__ out) {
     const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     const int64_t tile = i / th;   // gathered tile (rank-major), row r of it
     const int r = static_cast<int>(i - tile * th);
-    if (tile >= nranks * slots) return;
-    const int64_t rank = tile / slots, slot = tile - rank * slots;
+    if (tile >= nranks * nslots) return;
+    const int64_t rank = tile / nslots, slot = slot0 + (tile - rank * nslots);
     const int64_t g = slot * nranks + rank;   // < 2^30 (rt_render_tiles_device's bound)
     if (g >= static_cast<int64_t>(frames) * tiles_total) return;   // a padding slot
     const int f = static_cast<int>(g / tiles_total), t = static_cast<int>(g - static_cast<int64_t>(f) * tiles_total);
@@ -1865,13 +1849,9 @@ void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevW
 
 // LDS part of the traversal stack: lds_stack entries per lane (the rest overflows to global)
 inline size_t bvh_lds(const DevScene &s, int lanes = kBvhBlock) {
-    return sizeof(int32_t) * lanes * static_cast<size_t>(std::max(s.lds_stack, 1)) + sizeof(Bvh4Node) * static_cast<size_t>(s.top_nodes);
+    return sizeof(int32_t) * lanes * static_cast<size_t>(std::max(s.lds_stack, 1));
 }
-// The LDS node cache holds four-wide nodes: off for the other tree kernels.
-inline DevScene for_width(DevScene s, int W) {
-    if (W != 4) s.top_nodes = 0;
-    return s;
-}
+inline DevScene for_width(DevScene s, int) { return s; }
 
 // Grid cap of the per-step BVH kernels (resident size at 7 waves per SIMD: a grid-stride walk).
 constexpr int kMaxBvhGrid = 4096;
@@ -2064,13 +2044,14 @@ void launch_ray_triangle_pairs(const float *R, const float *T, int32_t n, uint8_
 }
 
 void launch_assemble_tiles(const uint8_t *gathered, int32_t width, int32_t height, int32_t tw, int32_t th, int32_t frames,
-                           int32_t nranks, uint8_t *out, hipStream_t stream) {
+                           int32_t nranks, uint8_t *out, hipStream_t stream, int64_t slot0, int64_t nslots) {
     const int32_t tiles_x = (width + tw - 1) / tw, tiles_total = tiles_x * ((height + th - 1) / th);
     const int64_t slots = (static_cast<int64_t>(frames) * tiles_total + nranks - 1) / nranks;
-    const int64_t rows = static_cast<int64_t>(nranks) * slots * th;   // one thread per gathered tile row
+    if (nslots < 0) nslots = slots - slot0;   // (default: the whole shard)
+    const int64_t rows = static_cast<int64_t>(nranks) * nslots * th;   // one thread per gathered tile row
     if (rows <= 0 || static_cast<int64_t>(frames) * width * height <= 0) return;
     hipLaunchKernelGGL(k_assemble_tiles, dim3(static_cast<unsigned>((rows + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
-                       gathered, width, height, tw, th, tiles_x, tiles_total, nranks, slots, frames, out);
+                       gathered, width, height, tw, th, tiles_x, tiles_total, nranks, slot0, nslots, frames, out);
 }
 
 }  // namespace rt
