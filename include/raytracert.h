@@ -278,18 +278,25 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
                                     and later ones use the faster (before that: on when the launch is at
                                     most two rounds of resident waves). C2 0.24 -> 0.18 ms, C3 -4%;
                                     C4 is faster without */
-#define RT_TUNE_STEAL_HALF 22    /* ordered launches of the stealing kernel: at most this many of the longest
-                                    batches (and at most 1/32 of them) run as two waves of 32 samples, the
-                                    other 32 lanes of each starting as helpers (default 512; 0 off; only
-                                    when 32 lanes hold whole pixels, i.e. pfx*pfy divides 32) */
+#define RT_TUNE_STEAL_HALF 22    /* ordered chain launches: at most this many of the longest batches (and at
+                                    most 1/32 of all, with the quarter and eighth tiers) run as two waves
+                                    of half the batch's pixels each, so the longest chains of a frame use
+                                    more SIMDs at once; in the stealing kernel the idle lanes of each start
+                                    as helpers (default 512; 0 off; needs >= 2 pixels per batch) */
 #define RT_TUNE_COLD_ESTIMATE 24 /* 1 (default): a fused launch over batches with no measured order (a new
                                     view's first frame) is ordered by a pre-pass that walks one primary
                                     ray per wave batch and scores the batch (walk cost, hit, shadows,
                                     reflective or refractive material); 0: screen order */
 #define RT_TUNE_FORGET_ORDER 25  /* any value: drop every measured batch order and wave-steal trial, so the
                                     next launch runs as a new view's first frame (benchmarks, tests) */
-#define RT_TUNE_STEAL_QUARTER 23 /* ... and before them this many of the longest run as four waves of 16
-                                    samples each (48 helpers per wave; default 0; pfx*pfy divides 16) */
+#define RT_TUNE_STEAL_QUARTER 23 /* ... and before them this many of the longest run as four waves of a
+                                    quarter of the pixels each (default 0; needs >= 4 pixels per batch) */
+#define RT_TUNE_SPLIT_EIGHTH 26  /* ... and before those this many as eight waves of an eighth of the pixels
+                                    (default 0; needs >= 8 pixels per batch) */
+#define RT_TUNE_PRIORITY_BATCHES 27 /* ordered chain launches: the waves of this many of the longest batches
+                                    (with their split parts) run at raised wave priority, so their
+                                    SIMDs issue them first (the longest batch is the frame's critical
+                                    path); default 0 */
 #define RT_TUNE_TOP_NODES 13     /* retired in r03 (0-85 accepted, no effect): an LDS copy of the four-wide
                                     tree's top levels; with float node rows loaded from global memory it
                                     measured slower (flat loads, 64-bit addresses) */

@@ -261,7 +261,7 @@ class Scene:
         """Launch-shape knobs ('xcd_split', 'bvh_grid', 'bvh_width', 'lds_stack', 'pipes',
         'shadow_virtual', 'pipe_batches', 'pipe_priority', 'chain_from', 'chain_split', 'top_nodes',
         'batch_order', 'order_every', 'fuse_pixels', 'wave_steal', 'steal_half', 'steal_quarter',
-        'cold_estimate', 'forget_order';
+        'cold_estimate', 'forget_order', 'split_eighth', 'prio_batches';
         retired, 0 only: 'wave_traversal', 'chain_refill', 'refill_grid'); outputs never depend on
         them."""
         k = {"xcd_split": _capi.TUNE_XCD_SPLIT, "bvh_grid": _capi.TUNE_BVH_GRID,
@@ -275,7 +275,8 @@ class Scene:
              "chain_refill": _capi.TUNE_CHAIN_REFILL, "refill_grid": _capi.TUNE_REFILL_GRID,
              "wave_steal": _capi.TUNE_WAVE_STEAL, "steal_half": _capi.TUNE_STEAL_HALF,
              "steal_quarter": _capi.TUNE_STEAL_QUARTER, "cold_estimate": _capi.TUNE_COLD_ESTIMATE,
-             "forget_order": _capi.TUNE_FORGET_ORDER}[knob]
+             "forget_order": _capi.TUNE_FORGET_ORDER, "split_eighth": _capi.TUNE_SPLIT_EIGHTH,
+             "prio_batches": _capi.TUNE_PRIORITY_BATCHES}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
 
     def batch_durations(self) -> np.ndarray:

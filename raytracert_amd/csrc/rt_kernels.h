@@ -85,6 +85,8 @@ struct DevScene {
     int32_t resident_grid;          // chain-kernel blocks resident on the device at once (CUs x blocks per CU)
     int32_t steal_half;             // RT_TUNE_STEAL_HALF: half-wave batches of the ordered stealing launch
     int32_t steal_quarter;          // RT_TUNE_STEAL_QUARTER: quarter-wave batches before them
+    int32_t split_eighth;           // RT_TUNE_SPLIT_EIGHTH: eighth-wave batches before those
+    int32_t prio_batches;           // RT_TUNE_PRIORITY_BATCHES: longest batches run at raised wave priority
 };
 
 struct DevWork {

@@ -1511,7 +1511,7 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
 template <int W, bool kAnyHit, bool kCount, bool kInLane = false, bool kSteal = false>
 __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kSteal ? RT_STEAL_WPE : RT_CHAIN_WPE))) void k_chain(
     const DevScene sc, const ShadeParams p, DevWork w, int first, int ordered, uint8_t *__restrict__ out_u8,
-    float *__restrict__ out_f32, int fuse_spp, int spb, int nbatch, const FrameGeom g, int split) {
+    float *__restrict__ out_f32, int fuse_spp, int spb, int nbatch, const FrameGeom g, int split, int split8) {
     extern __shared__ int32_t lds_stack[];
     __shared__ int s_q[kChainSteps], s_sh[kChainSteps];
     for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) { s_q[i] = 0; s_sh[i] = 0; }
@@ -1526,22 +1526,31 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         if (i0 == 0) w.counters[0] = nq;
     }
     if (!kInLane) nbatch = (nq + kWave - 1) / kWave;   // (spb = 64)
-    const int s2 = split & 0xFFFF, s4 = split >> 16, extra = 3 * s4 + s2;
+    const int s2 = split & 0xFFFF, s4 = split >> 16, extra = 7 * split8 + 3 * s4 + s2;
     const int lane = __lane_id();
+    const int spp = kInLane ? fuse_spp : 1, ppb = spb / spp;   // sample lanes per pixel, pixels per batch
     // pixel base lane of this lane's sample (fused launches): the first lane of its spp-lane group
     const int pix_lane = kInLane ? ((fuse_spp & (fuse_spp - 1)) == 0 ? (lane & ~(fuse_spp - 1)) : lane - lane % fuse_spp) : 0;
     drive_queries((nbatch + extra) * kWave, sc.chain_split & 3, w.wq + (2 * first) * kWqSlot, [&](int j0, int vend) {
         const int vb = j0 >> 6;   // this wave's virtual batch (wave-uniform for the orderable distributions)
-        const bool quarter = ordered && vb < 4 * s4;
-        const bool half = ordered && !quarter && vb - 4 * s4 < 2 * s2;
-        const int ob = quarter ? (vb >> 2) : half ? s4 + ((vb - 4 * s4) >> 1) : vb - (ordered ? extra : 0);
+        // split tiers of the order: 8 parts, then 4, then 2; part = which part of batch order[ob]
+        int ob = vb - (ordered ? extra : 0), nparts = 1, part = 0;
+        if (ordered) {
+            const int v4 = vb - 8 * split8, v2 = v4 - 4 * s4;
+            if (vb < 8 * split8) { nparts = 8; ob = vb >> 3; part = vb & 7; }
+            else if (v4 < 4 * s4) { nparts = 4; ob = split8 + (v4 >> 2); part = v4 & 3; }
+            else if (v2 < 2 * s2) { nparts = 2; ob = split8 + s4 + (v2 >> 1); part = v2 & 1; }
+        }
+        if (ordered) {   // the longest batches (and their parts) issue first on their SIMD
+            if (ob < sc.prio_batches) __builtin_amdgcn_s_setprio(3);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+        const int plen = ((ppb + nparts - 1) / nparts) * spp;   // whole pixels per part
         const bool wave_on = (vb << 6) < vend;
         const int pb = (ordered && wave_on) ? w.batch_order[ob] : vb;
-        const int lane_off = quarter ? ((vb & 3) * (kWave / 4) + lane)
-                           : half    ? (((vb - 4 * s4) & 1) * (kWave / 2) + lane) : (j0 & (kWave - 1));
+        const int lane_off = nparts > 1 ? part * plen + lane : (j0 & (kWave - 1));
         // (unordered, the XCD-segment distributions hand out unaligned ranges: the lane's own bound)
-        const bool lane_on = (ordered ? wave_on : j0 < vend) && (quarter ? lane < kWave / 4 : !half || lane < kWave / 2) &&
-                             lane_off < spb;
+        const bool lane_on = (ordered ? wave_on : j0 < vend) && (nparts == 1 || lane < plen) && lane_off < spb;
         const int j = pb * spb + lane_off;   // this lane's sample (kInLane) or queue entry
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         V3 rgb = mk(0, 0, 0);   // fused pixels: this lane's folded chain and its pixel (valid samples)
@@ -1591,7 +1600,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
             acc = mk(acc.x / div, acc.y / div, acc.z / div);   // operator/, Vec3D.h:36-38
             if (lane == pix_lane && px >= 0) store_pixel(acc, 3 * static_cast<int64_t>(px), out_u8, out_f32);
         }
-        if (lane == 0 && wave_on)
+        if (lane == 0 && wave_on)   // (a split batch: its parts' lifetimes, the last to finish stored)
             w.batch_cost[pb] = static_cast<uint32_t>(min(__builtin_amdgcn_s_memrealtime() - t0, 0xFFFFFFFFull));
     });
     wc.flush(sc.work);
@@ -1941,7 +1950,7 @@ int64_t chain_batches(int64_t capacity, int fuse_spp) {
 
 // k_chain's instantiations by width, any-hit shadows, work counting, fused frame and stealing
 typedef void (*ChainKernel)(const DevScene, const ShadeParams, DevWork, int, int, uint8_t *, float *, int, int, int,
-                            const FrameGeom, int);
+                            const FrameGeom, int, int);
 template <int W, bool kInLane, bool kSteal>
 ChainKernel chain_kernel(bool anyhit, bool count) {
     return anyhit ? (count ? k_chain<W, true, true, kInLane, kSteal> : k_chain<W, true, false, kInLane, kSteal>)
@@ -1965,20 +1974,23 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
                            : (wide ? chain_kernel<4, false, false>(anyhit, count) : chain_kernel<2, false, false>(anyhit, count));
     const int spb = fused ? chain_spb(fuse_spp) : kWave;
     const int64_t nbatch = fused ? chain_batches(capacity, fuse_spp) : (capacity + kWave - 1) / kWave;
-    // the stealing kernel, ordered over grid-stride batches: the longest batches run as quarter and
-    // half waves (at most 1/RT_STEAL_SPLIT_DIV of the batches together), when a part holds whole
-    // pixels (a pixel's sub-samples are summed within one wave's lanes)
-    int s2 = 0, s4 = 0;
-    if (steal && ordered && (s.chain_split & 3) == 0 && spb == kWave) {
-        const int64_t cap = nbatch / RT_STEAL_SPLIT_DIV;
-        if ((kWave / 4) % fuse_spp == 0) s4 = static_cast<int>(std::min<int64_t>(cap, s.steal_quarter));
-        if ((kWave / 2) % fuse_spp == 0) s2 = static_cast<int>(std::min<int64_t>(cap - s4, s.steal_half));
+    // ordered launches over grid-stride batches: the longest batches run as eighth, quarter and half
+    // waves (at most 1/RT_STEAL_SPLIT_DIV of the batches together; each part holds whole pixels, as
+    // a pixel's sub-samples are summed within one wave's lanes), so the longest chains of the frame
+    // run on more SIMDs at once; in the stealing kernel a part's idle lanes steal from its walks
+    int s2 = 0, s4 = 0, s8 = 0;
+    if (ordered && (s.chain_split & 3) == 0) {
+        const int ppb = spb / (fused ? fuse_spp : 1);
+        int64_t cap = nbatch / RT_STEAL_SPLIT_DIV;
+        if (ppb >= 8) { s8 = static_cast<int>(std::min<int64_t>(cap, s.split_eighth)); cap -= s8; }
+        if (ppb >= 4) { s4 = static_cast<int>(std::min<int64_t>(cap, s.steal_quarter)); cap -= s4; }
+        if (ppb >= 2) s2 = static_cast<int>(std::min<int64_t>(cap, s.steal_half));
     }
     const int split = s2 | (s4 << 16);
     const FrameGeom geom = g ? with_divisors(*g) : FrameGeom{};
-    hipLaunchKernelGGL(k, dim3(grid_bvh((nbatch + 3 * s4 + s2) * kWave, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s,
+    hipLaunchKernelGGL(k, dim3(grid_bvh((nbatch + 7 * s8 + 3 * s4 + s2) * kWave, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s,
                        p, w, first, ordered ? 1 : 0, out_u8, out_f32, fused ? fuse_spp : 0, spb, static_cast<int>(nbatch),
-                       geom, split);
+                       geom, split, s8);
 }
 
 void launch_estimate(const DevScene &s0, const ShadeParams &p, const FrameGeom &g, int fuse_spp, int64_t capacity,

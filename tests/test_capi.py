@@ -102,6 +102,7 @@ def test_tune_knobs_validate_ranges(tmp_path):
                             ("refill_grid", (0,), (1, 2560)), ("wave_traversal", (0,), (1, -1)),
                             ("batch_order", (0, 1), (2, 3)), ("chain_split", (0, 3), (4, 7)),
                             ("steal_half", (0, 512, 65535), (-1, 65536)), ("steal_quarter", (0, 8, 4096), (-1, 4097)),
+                            ("split_eighth", (0, 64, 4096), (-1, 4097)), ("prio_batches", (0, 64, 1 << 30), (-1,)),
                             ("pipes", (1, 4), (0, 5))]:
         for v in good:
             s.tune(knob, v)

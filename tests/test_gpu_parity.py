@@ -443,25 +443,28 @@ def test_wave_steal_matches_plain_walk(spec, w, h, pf, lights, workdir, gpu_avai
             assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
 
 
-@pytest.mark.parametrize("spec,w,h,pf,pfy,half,quarter", [("ref:dodgeColorTest.obj", 400, 300, 1, 1, 512, 8),
-                                                            ("ref:dodgeColorTest.obj", 200, 150, 1, 1, 0, 4096),
-                                                            ("syn:C4", 160, 90, 2, 2, 3, 5), ("syn:F4", 96, 54, 4, 4, 0, 2),
-                                                            ("syn:C4", 64, 36, 8, 8, 512, 8), ("syn:C4", 80, 45, 4, 8, 512, 8),
-                                                            ("syn:F4", 60, 34, 3, 3, 512, 8), ("syn:C4", 72, 40, 2, 8, 8, 8)])
-def test_steal_split_matches_plain_walk(spec, w, h, pf, pfy, half, quarter, workdir, gpu_available):
-    """RT_TUNE_STEAL_HALF / RT_TUNE_STEAL_QUARTER: in ordered launches of the stealing kernel the
-    longest batches run as four waves of 16 samples and the next as two of 32 when a part holds
-    whole pixels (pf 2 and 4: a pixel's sub-samples stay in adjacent lanes of one part); pf 8 x 8,
-    4 x 8 and 2 x 8 (64 and 32 and 16 sub-samples) and pf 3 (63-lane batches) must skip the parts
-    that would cut a pixel (a half-wave wrote half a pixel). Frames, floats and ray
-    counts equal the plain walk's on every launch (the first is unordered, later ones ordered)."""
+@pytest.mark.parametrize("spec,w,h,pf,pfy,steal,half,quarter,eighth", [
+    ("ref:dodgeColorTest.obj", 400, 300, 1, 1, 1, 512, 8, 0), ("ref:dodgeColorTest.obj", 200, 150, 1, 1, 1, 0, 4096, 0),
+    ("syn:C4", 160, 90, 2, 2, 1, 3, 5, 0), ("syn:F4", 96, 54, 4, 4, 1, 0, 2, 8),
+    ("syn:C4", 64, 36, 8, 8, 1, 512, 8, 8), ("syn:C4", 80, 45, 4, 8, 1, 512, 8, 8),
+    ("syn:F4", 60, 34, 3, 3, 1, 512, 8, 8), ("syn:C4", 72, 40, 2, 8, 1, 8, 8, 8),
+    ("ref:dodgeColorTest.obj", 400, 300, 1, 1, 0, 512, 16, 16), ("syn:C4", 333, 187, 3, 3, 0, 100, 50, 20),
+    ("syn:C4", 160, 90, 2, 2, 0, 8, 8, 8), ("syn:F4", 60, 34, 3, 3, 0, 0, 0, 4096)])
+def test_split_batches_match_plain_walk(spec, w, h, pf, pfy, steal, half, quarter, eighth, workdir, gpu_available):
+    """RT_TUNE_STEAL_HALF / _QUARTER / RT_TUNE_SPLIT_EIGHTH: in ordered chain launches (with and
+    without stealing) the longest batches run as eight, four or two waves of whole pixels each
+    (pf 3: 63-lane batches of 7 pixels split 4+3, 2+2+2+1, 1 x 7); pf 8 x 8 and 4 x 8 (one and two
+    pixels per batch) must skip the tiers that would cut a pixel (a half-wave wrote half
+    a pixel). Frames, floats and ray counts equal the plain walk's on every launch (the first is
+    unordered, later ones ordered, with a part's duration x parts recorded as the batch's cost)."""
     p = R.RenderParams(width=w, height=h, pf=pf, pfy=pfy, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
     with R.Scene.load(scene_path(spec, workdir), device=0) as sc:
         sc.tune("wave_steal", 0)
         ref, reff, refc = sc.render(p, want_f32=True)
-        sc.tune("wave_steal", 1)
+        sc.tune("wave_steal", steal)
         sc.tune("steal_half", half)
         sc.tune("steal_quarter", quarter)
+        sc.tune("split_eighth", eighth)
         for _ in range(4):
             u8, f32, c = sc.render(p, want_f32=True)
             assert [int(x) for x in c] == [int(x) for x in refc]

@@ -1,0 +1,65 @@
+"""Critical-path diagnostic: the longest wave batches of an ordered frame, re-rendered alone.
+
+For a workload of bench.py, renders warm frames, takes the per-batch wave lifetimes
+(rt_batch_durations), and re-renders each of the longest batches' pixel rectangles by themselves
+(an otherwise idle GPU): if a batch is as slow alone as inside the frame, its time is the latency
+of its own chains (walk iterations x load latency); if much faster, it is contention with the rest
+of the frame. Also prints the work counters (rays, node visits, triangle tests) of each rectangle.
+Usage: python tools/critical_path.py [workload] [n_longest]
+"""
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+import bench  # noqa: E402
+import raytracert_amd as R  # noqa: E402
+from raytracert_amd import _capi  # noqa: E402
+
+
+def main():
+    wl_name = sys.argv[1] if len(sys.argv) > 1 else "c4"
+    n_top = int(sys.argv[2]) if len(sys.argv) > 2 else 6
+    wl = bench.WORKLOADS[wl_name]
+    tile = 16
+    spp = wl["pf"] * wl["pf"]
+    spb = (64 // spp) * spp
+    with tempfile.TemporaryDirectory() as d:
+        path = bench.workload_scene(wl["scene"], d)
+        p = R.RenderParams(width=wl["width"], height=wl["height"], pf=wl["pf"], max_lvl=wl["max_lvl"],
+                           lights=[list(x) for x in wl["lights"]])
+        with R.Scene.load(path, device=0) as sc:
+            for _ in range(8):
+                sc.render(p)
+            dur = sc.batch_durations()
+            print(f"{wl_name}: {dur.size} batches, max {dur.max():.1f} us, p99 {np.percentile(dur, 99):.1f}, "
+                  f"median {np.median(dur):.1f}, sum {dur.sum() / 1e3:.1f} ms")
+            tiles_x = (wl["width"] + tile - 1) // tile
+            for b in np.argsort(dur)[::-1][:n_top]:
+                s0 = int(b) * spb   # first sample of the batch (tile-major, 16 x 16 tiles, spp per pixel)
+                pix0, pix1 = s0 // spp, (s0 + spb - 1) // spp
+                t, p0 = divmod(pix0, tile * tile)
+                ty, tx = divmod(t, tiles_x)
+                y0 = ty * tile + p0 // tile
+                y1 = ty * tile + (pix1 - t * tile * tile) // tile
+                x0 = tx * tile
+                rect = (x0, y0, tile, y1 - y0 + 1)
+                alone = []
+                for _ in range(4):
+                    sc.render(p, *rect)
+                    alone.append(float(sc.batch_durations().max()))
+                sc.reset_stats()
+                sc.set_profiling(True, count_work=True)
+                _, _, counts = sc.render(p, *rect)
+                sc.set_profiling(False)
+                ct, cv = sc.work_stats(_capi.KERNEL_CLOSEST_HIT)
+                st, sv = sc.work_stats(_capi.KERNEL_SHADOW)
+                print(f"  batch {int(b)}: {dur[b]:.1f} us in the frame; alone {min(alone):.1f}-{max(alone):.1f} us; "
+                      f"rect {rect}; rays {[int(c) for c in counts]}; closest visits {cv:.0f} tests {ct:.0f}; shadow visits {sv:.0f} tests {st:.0f}")
+
+
+if __name__ == "__main__":
+    main()
