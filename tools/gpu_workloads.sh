@@ -6,7 +6,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 TAG=${1:-r02}
-for W in c2 c3 c5 c5s; do
+for W in ref_default c2 c3 c5 c5s; do
   EXTRA="--no-bf-roofline"
   [ "$W" = "c5s" ] && EXTRA="$EXTRA --no-cpu"
   timeout -k 10 900 python bench.py --workload $W $EXTRA > gpurun_out/bench_${TAG}_$W.json 2> gpurun_out/bench_${TAG}_$W.err || { echo "bench $W failed"; tail -20 gpurun_out/bench_${TAG}_$W.err; exit 1; }
