@@ -297,6 +297,13 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
                                     (with their split parts) run at raised wave priority, so their
                                     SIMDs issue them first (the longest batch is the frame's critical
                                     path); default 0 */
+#define RT_TUNE_PIXEL_ORDER 28   /* which pixels of a tile share a wave batch (samples are tile-major):
+                                    0 row-major (a 64-sample batch of a 16x16 tile is 16x4 pixels),
+                                    1 Morton order in square power-of-two tiles (8x8 pixels at pf 1,
+                                    4x4 at pf 2: the rays of a batch stay closer together), 2 (default)
+                                    Morton when pfx*pfy is a power of two and the launch is not one the
+                                    stealing kernel may take (at most two rounds of resident waves),
+                                    else row-major. C4 0.465 -> 0.430 ms, C5 8.47 -> 7.09 ms */
 #define RT_TUNE_TOP_NODES 13     /* retired in r03 (0-85 accepted, no effect): an LDS copy of the four-wide
                                     tree's top levels; with float node rows loaded from global memory it
                                     measured slower (flat loads, 64-bit addresses) */

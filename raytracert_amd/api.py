@@ -261,7 +261,7 @@ class Scene:
         """Launch-shape knobs ('xcd_split', 'bvh_grid', 'bvh_width', 'lds_stack', 'pipes',
         'shadow_virtual', 'pipe_batches', 'pipe_priority', 'chain_from', 'chain_split', 'top_nodes',
         'batch_order', 'order_every', 'fuse_pixels', 'wave_steal', 'steal_half', 'steal_quarter',
-        'cold_estimate', 'forget_order', 'split_eighth', 'prio_batches';
+        'cold_estimate', 'forget_order', 'split_eighth', 'prio_batches', 'pixel_order';
         retired, 0 only: 'wave_traversal', 'chain_refill', 'refill_grid'); outputs never depend on
         them."""
         k = {"xcd_split": _capi.TUNE_XCD_SPLIT, "bvh_grid": _capi.TUNE_BVH_GRID,
@@ -276,7 +276,8 @@ class Scene:
              "wave_steal": _capi.TUNE_WAVE_STEAL, "steal_half": _capi.TUNE_STEAL_HALF,
              "steal_quarter": _capi.TUNE_STEAL_QUARTER, "cold_estimate": _capi.TUNE_COLD_ESTIMATE,
              "forget_order": _capi.TUNE_FORGET_ORDER, "split_eighth": _capi.TUNE_SPLIT_EIGHTH,
-             "prio_batches": _capi.TUNE_PRIORITY_BATCHES}[knob]
+             "prio_batches": _capi.TUNE_PRIORITY_BATCHES,
+             "pixel_order": _capi.TUNE_PIXEL_ORDER}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
 
     def batch_durations(self) -> np.ndarray:

@@ -26,6 +26,8 @@ struct FrameGeom {
     int32_t tiles_total;                // tiles per frame: ids wrap modulo this (multi-frame batches)
     int32_t stochastic;                 // RT_STOCHASTIC: jittered sub-samples
     uint32_t seed;                      // its hash seed
+    int32_t pix_order;                  // pixels of a tile in sample order: 0 row-major, 1 Morton (square
+                                        // power-of-two tiles: a 64-sample batch covers 8x8 pixels)
     float corners[8][3];                // origin00,dest00,origin01,dest01,origin10,dest10,origin11,dest11
     // divisions by the geometry, as multiply-high + shifts (fastdiv.h); the launchers fill them
     UDiv div_spp, div_tpx, div_tiles, div_tx, div_tw, div_pfy;

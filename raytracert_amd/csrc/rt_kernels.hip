@@ -1053,14 +1053,29 @@ __global__ __launch_bounds__(kBlock) void k_intersect_only(const TriRec *__restr
 // Sample generation: main.cpp:377-386 for every sub-sample of the batch's tiles.
 // ---------------------------------------------------------------------------------------------
 // (Indices are below 2^31: batches are capped at 2^30 samples and tile ids at 2^30, rt_capi.cpp.)
-__device__ __forceinline__ bool decode_pixel(const FrameGeom &g, int64_t pix64, int &x, int &y) {
+// The even bits of v packed into its low half (Morton decode of one coordinate).
+__device__ __forceinline__ uint32_t compact_bits(uint32_t v) {
+    v &= 0x55555555u;
+    v = (v | (v >> 1)) & 0x33333333u;
+    v = (v | (v >> 2)) & 0x0F0F0F0Fu;
+    v = (v | (v >> 4)) & 0x00FF00FFu;
+    return (v | (v >> 8)) & 0x0000FFFFu;
+}
+
+// Pixel pix of a batch (tile-major: tile tl = pix / (tw th), then the tile's pixels in g.pix_order):
+// its frame position and its slot in the tile-major shard layout, where a tile is always row-major
+// (rt_assemble_tiles_device's layout, whatever order the samples take).
+__device__ __forceinline__ bool decode_pixel(const FrameGeom &g, int64_t pix64, int &x, int &y, uint32_t &slot) {
     const uint32_t pix = static_cast<uint32_t>(pix64);
     const uint32_t tl = udiv(pix, g.div_tpx);
     const uint32_t p = pix - tl * g.div_tpx.d;
     const uint32_t tid = umod(static_cast<uint32_t>(g.first) + (static_cast<uint32_t>(g.tile0) + tl) * static_cast<uint32_t>(g.stride),
                               g.div_tiles);
     const uint32_t ty = udiv(tid, g.div_tx), tx = tid - ty * g.div_tx.d;
-    const uint32_t py = udiv(p, g.div_tw), pxl = p - py * g.div_tw.d;
+    uint32_t py, pxl;
+    if (g.pix_order) { pxl = compact_bits(p); py = compact_bits(p >> 1); }   // Morton (tw = th = 2^k)
+    else { py = udiv(p, g.div_tw); pxl = p - py * g.div_tw.d; }
+    slot = tl * g.div_tpx.d + py * g.div_tw.d + pxl;
     x = g.ox + static_cast<int>(tx) * g.tw + static_cast<int>(pxl);
     y = g.oy + static_cast<int>(ty) * g.th + static_cast<int>(py);
     return x < g.width && y < g.height && x < g.ox + g.cw && y < g.oy + g.ch && x >= 0 && y >= 0;
@@ -1084,8 +1099,9 @@ __device__ __forceinline__ bool primary_sample(const FrameGeom &g, int64_t s, V3
     const int subx = static_cast<int>(udiv(static_cast<uint32_t>(sub), g.div_pfy));
     const int suby = sub - subx * g.pfy;   // subx outer, suby inner (:377-378)
     int x, y;
-    const bool valid = decode_pixel(g, pix, x, y);
-    px = g.out_mode == 0 ? static_cast<int64_t>(g.tile0) * g.tw * g.th + pix
+    uint32_t slot;
+    const bool valid = decode_pixel(g, pix, x, y, slot);
+    px = g.out_mode == 0 ? static_cast<int64_t>(g.tile0) * g.tw * g.th + slot
                          : static_cast<int64_t>(y - g.oy) * g.cw + (x - g.ox);
     origin = mk(0, 0, 0);
     dest = mk(0, 0, 0);
@@ -1660,10 +1676,11 @@ __global__ __launch_bounds__(kBlock) void k_frame(const FrameGeom g, DevWork w, 
     const int64_t pix = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (pix >= npix) return;
     int x, y;
-    const bool valid = decode_pixel(g, pix, x, y);
+    uint32_t slot;
+    const bool valid = decode_pixel(g, pix, x, y, slot);
     const int spp = g.pfx * g.pfy;
     int64_t o;
-    if (g.out_mode == 0) o = 3 * (static_cast<int64_t>(g.tile0) * g.tw * g.th + pix);
+    if (g.out_mode == 0) o = 3 * (static_cast<int64_t>(g.tile0) * g.tw * g.th + slot);
     else o = 3 * (static_cast<int64_t>(y - g.oy) * g.cw + (x - g.ox));
     if (!valid) {
         if (g.out_mode == 0 && out_u8) { out_u8[o] = 0; out_u8[o + 1] = 0; out_u8[o + 2] = 0; }

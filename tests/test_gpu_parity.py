@@ -199,6 +199,43 @@ def test_fused_pixel_writes_equal_frame_pass(spec, size, pf, want_f32, workdir, 
     assert np.array_equal(a[4], b[4])
 
 
+@pytest.mark.parametrize("spec,size,pf,tile", [("syn:F3", (100, 70), 1, 16), ("syn:F3", (100, 70), 2, 16),
+                                               ("syn:F3", (61, 29), 3, 16), ("syn:F4", (37, 23), 4, 8),
+                                               ("syn:C4", (1920, 1080), 1, 16), ("syn:F3", (100, 70), 1, 32),
+                                               ("syn:F3", (100, 70), 2, 12)])
+def test_pixel_order_keeps_results(spec, size, pf, tile, workdir, gpu_available):
+    """RT_TUNE_PIXEL_ORDER only changes which pixels share a wave batch: row-major, Morton (square
+    power-of-two tiles; a 12x12 tile stays row-major) and auto give the same frame (the row-major
+    device frame, the tile-major shard layout with its rows un-permuted as before, the rectangle
+    render) and the same ray counts, cold and batch-ordered, with the fused frame and the frame pass."""
+    import torch
+    w, h = size
+    p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=3, lights=[[0, 0, 4], [1.5, 1.5, 4]])
+    ntiles = ((w + tile - 1) // tile) * ((h + tile - 1) // tile)
+    stream = torch.cuda.current_stream().cuda_stream
+    out = {}
+    with R.Scene.load(scene_path(spec, workdir), device=0) as sc:
+        for fuse in (1, 0):
+            sc.tune("fuse_pixels", fuse)
+            for order in (0, 1, 2):
+                sc.tune("pixel_order", order)
+                sc.tune("forget_order", 1)
+                for rep in range(2):   # cold, then ordered by the first launch's durations
+                    fb = torch.full((h * w * 3,), 7, dtype=torch.uint8, device="cuda:0")
+                    c = sc.render_frame_device(p, tile, tile, fb.data_ptr(), fb.numel(), stream, want_counts=True)
+                    tb = torch.full((ntiles * tile * tile * 3,), 7, dtype=torch.uint8, device="cuda:0")
+                    n, tc = sc.render_tiles_device(p, tile, tile, 0, 1, tb.data_ptr(), tb.numel(), stream, want_counts=True)
+                    assert n == ntiles
+                    out[(fuse, order, rep)] = (fb.cpu().numpy(), tb.cpu().numpy(), [int(x) for x in c], [int(x) for x in tc])
+        u8, _, counts = sc.render(p)
+    ref = out[(0, 0, 0)]
+    assert np.array_equal(ref[0].reshape(h, w, 3), u8) and ref[2] == [int(x) for x in counts]
+    for key, v in out.items():
+        assert np.array_equal(v[0], ref[0]), key
+        assert np.array_equal(v[1], ref[1]), key
+        assert v[2] == ref[2] and v[3] == ref[2], key
+
+
 def test_transparent_shadow_path_and_deep_chain(workdir, gpu_available):
     """F4 scenes exercise the closest-hit shadow path (a transparent material exists) and
     chains deeper than 2; the golden comparison above covers bytes, this checks counts against

@@ -38,15 +38,25 @@ def main():
             print(f"{wl_name}: {dur.size} batches, max {dur.max():.1f} us, p99 {np.percentile(dur, 99):.1f}, "
                   f"median {np.median(dur):.1f}, sum {dur.sum() / 1e3:.1f} ms")
             tiles_x = (wl["width"] + tile - 1) // tile
+            # pixel order in a tile (RT_TUNE_PIXEL_ORDER auto): Morton unless the launch may steal
+            morton = wl["width"] * wl["height"] * spp > 2 * R.device_resident_lanes() if hasattr(R, "device_resident_lanes") \
+                else int(os.environ.get("RT_CRIT_MORTON", "1"))
+
+            def pixel_xy(pix):
+                t, q = divmod(pix, tile * tile)
+                ty, tx = divmod(t, tiles_x)
+                if morton:
+                    px = sum(((q >> (2 * k)) & 1) << k for k in range(8))
+                    py = sum(((q >> (2 * k + 1)) & 1) << k for k in range(8))
+                else:
+                    py, px = divmod(q, tile)
+                return tx * tile + px, ty * tile + py
+
             for b in np.argsort(dur)[::-1][:n_top]:
                 s0 = int(b) * spb   # first sample of the batch (tile-major, 16 x 16 tiles, spp per pixel)
-                pix0, pix1 = s0 // spp, (s0 + spb - 1) // spp
-                t, p0 = divmod(pix0, tile * tile)
-                ty, tx = divmod(t, tiles_x)
-                y0 = ty * tile + p0 // tile
-                y1 = ty * tile + (pix1 - t * tile * tile) // tile
-                x0 = tx * tile
-                rect = (x0, y0, tile, y1 - y0 + 1)
+                xy = [pixel_xy(q) for q in range(s0 // spp, (s0 + spb - 1) // spp + 1)]
+                x0, y0 = min(v[0] for v in xy), min(v[1] for v in xy)
+                rect = (x0, y0, max(v[0] for v in xy) - x0 + 1, max(v[1] for v in xy) - y0 + 1)
                 alone = []
                 for _ in range(4):
                     sc.render(p, *rect)
