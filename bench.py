@@ -321,9 +321,9 @@ def main():
                      "all_equal_one_gpu_frame": bool(all(torch.equal(frames[f], ref) for f in range(frames.shape[0]))),
                      "note": "ranks share one GPU; gloo host-staged gather: logic check, not a scaling number"}
 
-    # ---- a cold frame: the first frame of a new view (no measured batch order, no steal trial):
-    # the library orders it by its primary-walk estimate (RT_TUNE_COLD_ESTIMATE); for comparison
-    # the same frame dispatched in screen order ----
+    # ---- a cold frame: the first frame of a new view (no measured batch order, no launch trial):
+    # the library dispatches it centre-out (RT_TUNE_COLD_ESTIMATE 2); for comparison the same frame
+    # dispatched in screen order ----
     def cold_frame(i):
         torch.cuda.synchronize(dev)
         if world > 1:
@@ -335,10 +335,11 @@ def main():
         torch.cuda.synchronize(dev)
         return time.perf_counter() - t0
 
+    trials = scene.trials() if hasattr(R._capi.lib(), "rt_scene_trials") else None   # the timed loop's launch shape
     cold = [cold_frame(i) for i in range(0 if args.no_cold else 3)]
     scene.tune("cold_estimate", 0)
     cold_screen = [cold_frame(i) for i in range(0 if args.no_cold else 3)]
-    scene.tune("cold_estimate", 1)
+    scene.tune("cold_estimate", 2)   # (the library default)
     cold_ms = sorted(cold)[1] * 1e3 if cold else None
     cold_screen_ms = sorted(cold_screen)[1] * 1e3 if cold_screen else None
     main_run.run(0, max(args.warmup, 3))   # re-learn the measured order before the other legs
@@ -498,9 +499,10 @@ def main():
                 "rays_by_kind_per_step": {"primary": rays_by_kind[0], "secondary": rays_by_kind[1], "shadow": rays_by_kind[2]},
                 "frame_ms_per_gpu": round(elapsed / args.steps * 1e3, 3),
                 "first_frame_ms": round(cold_ms, 3) if cold_ms is not None else None,
-                "first_frame_what": "a new view's first frame (no measured batch order or steal trial: every order "
-                                    "forgotten first), ordered by the library's primary-walk estimate, median of 3, "
-                                    "synchronised",
+                "first_frame_what": "a new view's first frame (no measured batch order or launch trial: every order "
+                                    "forgotten first), dispatched centre-out (RT_TUNE_COLD_ESTIMATE 2) as dynamic "
+                                    "wave tasks (RT_TUNE_CHAIN_SPLIT 5), median of 3, synchronised, host wall clock",
+                "launch_trials": trials,
                 "first_frame_screen_order_ms": round(cold_screen_ms, 3) if cold_screen_ms is not None else None,
                 "scene_load_s": round(t_load, 3), "scene_gen_s": round(t_gen, 3),
             },

@@ -283,10 +283,11 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
                                     of half the batch's pixels each, so the longest chains of a frame use
                                     more SIMDs at once; in the stealing kernel the idle lanes of each start
                                     as helpers (default 512; 0 off; needs >= 2 pixels per batch) */
-#define RT_TUNE_COLD_ESTIMATE 24 /* 1 (default): a fused launch over batches with no measured order (a new
-                                    view's first frame) is ordered by a pre-pass that walks one primary
-                                    ray per wave batch and scores the batch (walk cost, hit, shadows,
-                                    reflective or refractive material); 0: screen order */
+#define RT_TUNE_COLD_ESTIMATE 24 /* how a fused launch over batches with no measured order (a new view's
+                                    first frame) is ordered: 2 (default) centre-out, by the distance of
+                                    each batch from the frame's centre (no walk); 1 a pre-pass that walks
+                                    one primary ray per wave batch and scores the batch; 0 screen order.
+                                    C4 cold frame 0.62 / 0.70 / 0.63 ms, C2 0.20 / 0.23 / 0.23 */
 #define RT_TUNE_FORGET_ORDER 25  /* any value: drop every measured batch order and wave-steal trial, so the
                                     next launch runs as a new view's first frame (benchmarks, tests) */
 #define RT_TUNE_STEAL_QUARTER 23 /* ... and before them this many of the longest run as four waves of a
@@ -304,12 +305,21 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
                                     Morton when pfx*pfy is a power of two and the launch is not one the
                                     stealing kernel may take (at most two rounds of resident waves),
                                     else row-major. C4 0.465 -> 0.430 ms, C5 8.47 -> 7.09 ms */
+#define RT_TUNE_DYN_GROUP 29     /* RT_TUNE_CHAIN_SPLIT 4: 2^value consecutive wave tasks (of the batch order)
+                                    go to one XCD before the next XCD's turn (default 2: four, as four
+                                    consecutive 64-thread waves of a 256-thread block) */
 #define RT_TUNE_TOP_NODES 13     /* retired in r03 (0-85 accepted, no effect): an LDS copy of the four-wide
                                     tree's top levels; with float node rows loaded from global memory it
                                     measured slower (flat loads, 64-bit addresses) */
 #define RT_TUNE_CHAIN_SPLIT 12   /* query distribution of the chain launch: as RT_TUNE_XCD_SPLIT, or 3: 64-query
                                     chunks dealt round-robin to the XCDs and taken dynamically within
-                                    each */
+                                    each, or 4 (fused frame launches; others use 0): a resident grid
+                                    whose waves each take a first wave batch by position and later ones
+                                    from per-XCD counters (RT_TUNE_DYN_GROUP consecutive batches per
+                                    XCD), in batch order once one is measured, so no wave slot waits for
+                                    the rest of its block to retire; 5 (default, auto): 4 for a cold
+                                    launch, then the per-view trials (RT_TUNE_WAVE_STEAL) also time 0
+                                    against 4 and keep the faster (rt_scene_trials) */
 #define RT_TUNE_PIPE_BATCHES 6     /* split a call into at least pipes x this many batches */
 #define RT_TUNE_PIPE_PRIORITY 7    /* 1 (default): pipelines after the first run at lower stream priority */
 #define RT_TUNE_SHADOW_VIRTUAL 5   /* bit k: step k's shadow rays are read from its hits directly
@@ -351,6 +361,12 @@ int rt_work_detail(rt_scene *scene, int32_t kind, uint64_t out[RT_WORK_FIELDS]);
  * and stamp builds were retired with the variants they measured); 0 in production builds.
  * Reads count words from offset (offset + count <= 131072); synchronises the device. */
 int rt_diag_read(rt_scene *scene, int64_t offset, int64_t count, uint64_t *out);
+/* The per-view launch trials of render pipeline 0 (RT_TUNE_WAVE_STEAL 2 x RT_TUNE_CHAIN_SPLIT 5):
+ * info = {trials timed (0 while pending), chosen trial (-1 pending), its wave_steal, its chain
+ * distribution}; trial_ms (may be NULL) = each trial's chain-launch time (trial t: steal t % ns,
+ * distribution t / ns, ns = 2 when both steal options are tried). Diagnostics; placement only. */
+int rt_scene_trials(rt_scene *scene, int32_t info[4], float trial_ms[4]);
+
 /* Per wave batch of the scene's latest chain launch (pipeline 0): the wave's duration in 100 MHz
  * ticks (s_memrealtime), in batch order (screen order of the batches, not dispatch order). *n_out =
  * the number of batches; up to capacity are copied. Synchronises the device. The longest batch is the

@@ -41,7 +41,7 @@ TUNE_CHAIN_SPLIT, TUNE_TOP_NODES, TUNE_BATCH_ORDER, TUNE_ORDER_EVERY, TUNE_FUSE_
 TUNE_CHAIN_REFILL, TUNE_REFILL_GRID, TUNE_WAVE_STEAL = 19, 20, 21
 TUNE_COLD_ESTIMATE, TUNE_FORGET_ORDER = 24, 25
 TUNE_STEAL_HALF, TUNE_STEAL_QUARTER = 22, 23
-TUNE_SPLIT_EIGHTH, TUNE_PRIORITY_BATCHES, TUNE_PIXEL_ORDER = 26, 27, 28
+TUNE_SPLIT_EIGHTH, TUNE_PRIORITY_BATCHES, TUNE_PIXEL_ORDER, TUNE_DYN_GROUP = 26, 27, 28, 29
 BVH_INFO_FIELDS = 7
 STOCHASTIC = 1 << 8
 DEFAULT_SEED = 0x5EED
@@ -114,6 +114,7 @@ _SIGNATURES = {
     "rt_diag_read": ([_VP, C.c_int64, C.c_int64, _VP], C.c_int),
     "rt_workspace_layout": ([C.c_int64, C.c_int32, C.c_int32, C.POINTER(C.c_uint64), _VP], C.c_int),
     "rt_batch_durations": ([_VP, _VP, C.c_int64, C.POINTER(C.c_int64)], C.c_int),
+    "rt_scene_trials": ([_VP, _VP, _VP], C.c_int),
     "rt_scene_bvh_digest": ([_VP, C.POINTER(C.c_uint64)], C.c_int),
     "rt_scene_bvh_validate": ([_VP], C.c_int),
     "rt_bvh_acceptance_box": ([_VP, _VP, _VP], C.c_int),

@@ -88,6 +88,8 @@ struct DevScene {
     int32_t steal_half;             // RT_TUNE_STEAL_HALF: half-wave batches of the ordered stealing launch
     int32_t steal_quarter;          // RT_TUNE_STEAL_QUARTER: quarter-wave batches before them
     int32_t split_eighth;           // RT_TUNE_SPLIT_EIGHTH: eighth-wave batches before those
+    int32_t cold_estimate;          // RT_TUNE_COLD_ESTIMATE: 1 primary-walk score, 2 centre-out
+    int32_t dyn_group_log2;         // RT_TUNE_DYN_GROUP: log2 of the consecutive wave tasks dealt to one XCD
     int32_t prio_batches;           // RT_TUNE_PRIORITY_BATCHES: longest batches run at raised wave priority
 };
 
@@ -116,6 +118,10 @@ constexpr int kWorkFields = 6;               // = RT_WORK_FIELDS
 constexpr int kDiagWords = 1 << 17;          // diagnostic words after the work counters (rt_diag_read)
 constexpr int kWqStride = 16;                // one 64-B line per segment counter
 constexpr int kWqSlot = 8 * kWqStride;       // eight segments (one per XCD) per launch
+// RT_TUNE_CHAIN_SPLIT 4 (fused chain launches): the eight per-XCD wave-task counters live in the
+// counter buffer, below the step counters' upper half, so the launch before (or k_gen_primary) has
+// zeroed them with the rest; max_lvl <= 254 keeps the step counters below this slot.
+constexpr int kWaveQueueSlot = kMaxStepsCounters - kWqSlot;
 
 // Launchers (all asynchronous on `stream`).
 // k_gen_primary zeroes w.counters (then counter 0 = the batch's samples) and w.wq, and writes the

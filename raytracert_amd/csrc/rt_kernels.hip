@@ -810,10 +810,10 @@ struct WorkTally {
 // from the others in turn, so no XCD idles while another has work. Every wave leaves after it has
 // seen all eight segments empty. Placement only changes speed, never results.
 struct QueryCursor {
-    int n, split, k = 0, base, step, end;
+    int n, split, k = 0, base, step, end, glog;
     int32_t *wq;
-    __device__ __forceinline__ QueryCursor(int n_, int split_, int32_t *wq_) : n(n_), split(split_), wq(wq_) {
-        if ((split == 2 || split == 3) && wq) return;
+    __device__ __forceinline__ QueryCursor(int n_, int split_, int32_t *wq_, int glog_ = 0) : n(n_), split(split_), glog(glog_), wq(wq_) {
+        if ((split == 2 || split == 3 || split == 4) && wq) return;
         const Segment seg = xcd_segment(n, kBvhBlock, split == 1);
         base = seg.start - seg.step;
         step = seg.step;
@@ -821,11 +821,34 @@ struct QueryCursor {
     }
     // Next query index for this lane (may be >= end: inactive lane); false once the wave is done.
     __device__ __forceinline__ bool next(int &j) {
-        if (split == 3 && wq) {   // 64-query chunks dealt round-robin to the XCDs, taken dynamically within each
-            const int g = blockIdx.x % kXcds;
+        if (split == 4 && wq) {   // as 3, but every wave's first chunk is static (its own slot in its XCD's
+            // sequence) and only later ones come from the counter, which then counts from the XCD's wave
+            // count: a launch's waves do not queue on eight counter words to get their first chunk
+            const int nx = min(kXcds, static_cast<int>(gridDim.x));   // (grids of fewer blocks: fewer sequences)
+            const int g = blockIdx.x % nx;
+            const int wpb = static_cast<int>(blockDim.x) / kWave;
+            int c;
+            if (k == 0) {
+                c = static_cast<int>(blockIdx.x / nx) * wpb + static_cast<int>(threadIdx.x) / kWave;
+                k = 1;
+            } else {
+                const int nblk = (static_cast<int>(gridDim.x) - 1 - g) / nx + 1;   // blocks of this sequence
+                int a = 0;
+                if (__lane_id() == 0) a = atomicAdd(&wq[g * kWqStride], 1);
+                c = nblk * wpb + __shfl(a, 0);
+            }
+            const int b = ((((c >> glog) * nx + g) << glog) + (c & ((1 << glog) - 1))) * kWave;
+            end = n;
+            if (b < n) { j = b + __lane_id(); return true; }
+            return false;
+        }
+        if (split == 3 && wq) {   // 64-query chunks dealt round-robin to the XCDs (in groups of 2^glog consecutive
+            const int nx = min(kXcds, static_cast<int>(gridDim.x));   // chunks), taken dynamically within each
+            const int g = blockIdx.x % nx;
             int c = 0;
             if (__lane_id() == 0) c = atomicAdd(&wq[g * kWqStride], 1);
-            const int b = (__shfl(c, 0) * kXcds + g) * kWave;
+            c = __shfl(c, 0);
+            const int b = ((((c >> glog) * nx + g) << glog) + (c & ((1 << glog) - 1))) * kWave;
             end = n;
             if (b < n) { j = b + __lane_id(); return true; }
             return false;
@@ -852,8 +875,8 @@ struct QueryCursor {
 };
 
 template <typename F>
-__device__ __forceinline__ void drive_queries(int n, int split, int32_t *__restrict__ wq, F &&body) {
-    QueryCursor c(n, split, wq);
+__device__ __forceinline__ void drive_queries(int n, int split, int32_t *__restrict__ wq, F &&body, int glog = 0) {
+    QueryCursor c(n, split, wq, glog);
     int j;
     while (c.next(j)) body(j, c.end);
 }
@@ -1547,7 +1570,12 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
     const int spp = kInLane ? fuse_spp : 1, ppb = spb / spp;   // sample lanes per pixel, pixels per batch
     // pixel base lane of this lane's sample (fused launches): the first lane of its spp-lane group
     const int pix_lane = kInLane ? ((fuse_spp & (fuse_spp - 1)) == 0 ? (lane & ~(fuse_spp - 1)) : lane - lane % fuse_spp) : 0;
-    drive_queries((nbatch + extra) * kWave, sc.chain_split & 3, w.wq + (2 * first) * kWqSlot, [&](int j0, int vend) {
+    // distribution 4 (fused launches): wave tasks dealt round-robin to the XCDs and taken one at a
+    // time from per-XCD counters in the (self-reset) counter buffer by a resident grid, so no wave
+    // slot waits for the other waves of its block to retire; in batch order when ordered
+    const bool dyn = kInLane && sc.chain_split == 4;
+    drive_queries((nbatch + extra) * kWave, dyn ? 4 : (sc.chain_split & 3), dyn ? &w.counters[kWaveQueueSlot] : w.wq + (2 * first) * kWqSlot,
+                  [&](int j0, int vend) {
         const int vb = j0 >> 6;   // this wave's virtual batch (wave-uniform for the orderable distributions)
         // split tiers of the order: 8 parts, then 4, then 2; part = which part of batch order[ob]
         int ob = vb - (ordered ? extra : 0), nparts = 1, part = 0;
@@ -1618,7 +1646,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         }
         if (lane == 0 && wave_on)   // (a split batch: its parts' lifetimes, the last to finish stored)
             w.batch_cost[pb] = static_cast<uint32_t>(min(__builtin_amdgcn_s_memrealtime() - t0, 0xFFFFFFFFull));
-    });
+    }, dyn ? sc.dyn_group_log2 : 0);
     wc.flush(sc.work);
     ws.flush(sc.work ? sc.work + kWorkFields : nullptr);
     __syncthreads();
@@ -1665,6 +1693,24 @@ __global__ __launch_bounds__(kBvhBlock) void k_estimate(const DevScene sc, const
         if (p.max_lvl > 0 && (refl || refr)) s *= 1 + static_cast<uint32_t>(min(p.max_lvl, 3));
     }
     score[b] = s;
+}
+
+// Center-out cold order (RT_TUNE_COLD_ESTIMATE 2): no walk at all; a batch scores by the distance of
+// its middle pixel from the frame's centre (score 2^30 / (1 + d^2 / 64), pixels), so the sort starts
+// the frame from the middle outward, where a view's subject and its long reflection chains usually
+// are. Placement only, like the walk estimate.
+__global__ __launch_bounds__(kBlock) void k_estimate_center(const FrameGeom g, int spb, int nbatch, uint32_t *__restrict__ score) {
+    const int b = static_cast<int>(blockIdx.x) * kBlock + static_cast<int>(threadIdx.x);
+    if (b >= nbatch) return;
+    const int64_t nq = static_cast<int64_t>(g.ntiles) * g.tw * g.th * g.pfx * g.pfy;
+    const int64_t first = static_cast<int64_t>(b) * spb, n = min(static_cast<int64_t>(spb), nq - first);
+    const uint32_t pix = udiv(static_cast<uint32_t>(first + n / 2), g.div_spp);
+    int x, y;
+    uint32_t slot;
+    decode_pixel(g, pix, x, y, slot);
+    const float dx = static_cast<float>(x) + 0.5f - 0.5f * static_cast<float>(g.width);
+    const float dy = static_cast<float>(y) + 0.5f - 0.5f * static_cast<float>(g.height);
+    score[b] = static_cast<uint32_t>(1073741824.0f / (1.0f + (dx * dx + dy * dy) * (1.0f / 64.0f)));
 }
 
 
@@ -2005,7 +2051,9 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
     }
     const int split = s2 | (s4 << 16);
     const FrameGeom geom = g ? with_divisors(*g) : FrameGeom{};
-    hipLaunchKernelGGL(k, dim3(grid_bvh((nbatch + 7 * s8 + 3 * s4 + s2) * kWave, s.bvh_grid)), dim3(kBvhBlock), bvh_lds(s), stream, s,
+    // distribution 4 (dynamic wave tasks): a resident grid, each wave takes tasks until none remain
+    const int grid_cap = (fused && s.chain_split == 4) ? std::max(1, std::min(s.bvh_grid, s.resident_grid)) : s.bvh_grid;
+    hipLaunchKernelGGL(k, dim3(grid_bvh((nbatch + 7 * s8 + 3 * s4 + s2) * kWave, grid_cap)), dim3(kBvhBlock), bvh_lds(s), stream, s,
                        p, w, first, ordered ? 1 : 0, out_u8, out_f32, fused ? fuse_spp : 0, spb, static_cast<int>(nbatch),
                        geom, split, s8);
 }
@@ -2014,6 +2062,11 @@ void launch_estimate(const DevScene &s0, const ShadeParams &p, const FrameGeom &
                      uint32_t *score, hipStream_t stream) {
     const int64_t nbatch = chain_batches(capacity, fuse_spp);
     if (nbatch <= 0) return;
+    if (s0.cold_estimate == 2) {
+        hipLaunchKernelGGL(k_estimate_center, dim3(grid_for(nbatch)), dim3(kBlock), 0, stream, with_divisors(g),
+                           chain_spb(fuse_spp), static_cast<int>(nbatch), score);
+        return;
+    }
     const bool wide = s0.bvh_width == 4;
     const DevScene s = for_width(s0, wide ? 4 : 2);
     const unsigned grid = static_cast<unsigned>((nbatch + kBvhBlock - 1) / kBvhBlock);

@@ -100,7 +100,9 @@ def test_tune_knobs_validate_ranges(tmp_path):
     s = R.Scene.load(str(p), device=R.RT_HOST_ONLY)
     for knob, good, bad in [("wave_steal", (0, 1, 2), (-1, 3)), ("chain_refill", (0,), (1,)),
                             ("refill_grid", (0,), (1, 2560)), ("wave_traversal", (0,), (1, -1)),
-                            ("batch_order", (0, 1), (2, 3)), ("chain_split", (0, 3), (4, 7)),
+                            ("batch_order", (0, 1), (2, 3)), ("chain_split", (0, 3, 4, 5), (6, 7, -1)),
+                            ("pixel_order", (0, 1, 2), (3, -1)), ("dyn_group", (0, 2, 6), (7, -1)),
+                            ("cold_estimate", (0, 1, 2), (3, -1)),
                             ("steal_half", (0, 512, 65535), (-1, 65536)), ("steal_quarter", (0, 8, 4096), (-1, 4097)),
                             ("split_eighth", (0, 64, 4096), (-1, 4097)), ("prio_batches", (0, 64, 1 << 30), (-1,)),
                             ("pipes", (1, 4), (0, 5))]:

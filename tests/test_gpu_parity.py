@@ -317,13 +317,14 @@ def test_render_accel_modes_match_golden(name, accel, workdir, gpu_available):
     _assert_image_close(u8, f32, gu8, gf32)
 
 
-@pytest.mark.parametrize("split", [0, 3])
+@pytest.mark.parametrize("split", [0, 3, 4, 5])
 @pytest.mark.parametrize("chain_from", [0, 1, 2, 255])
 @pytest.mark.parametrize("name", ["F2_dodge_200x150", "F2b_shadow_test_160x120", "F3_spheres_128x72_pf2",
                                   "F4_refract_128x72"])
 def test_chain_tail_matches_golden(name, chain_from, split, workdir, gpu_available):
     """The per-lane chain launch (RT_TUNE_CHAIN_FROM) from the first step, from the second, and
-    never, with grid-stride and dynamic (RT_TUNE_CHAIN_SPLIT 3) query distribution: the golden
+    never, with grid-stride, dynamic (RT_TUNE_CHAIN_SPLIT 3), dynamic fused-launch wave tasks (4)
+    and the per-launch auto choice (5) as query distribution: the golden
     frames and ray counts each time. F4 has transparent materials, so its shadow rays take the
     closest-hit form; dodgeColorTest has always-list triangles."""
     entry = golden_index()[name]
@@ -381,8 +382,9 @@ def test_batch_order_from_previous_launch_keeps_results(mode, pf, size, workdir,
 @pytest.mark.parametrize("spec,w,h,pf", [("syn:C4", 320, 180, 1), ("ref:dodgeColorTest.obj", 200, 150, 3),
                                          ("syn:F4", 96, 54, 2), ("syn:F4", 17, 9, 1)])
 def test_cold_estimate_order_keeps_results(spec, w, h, pf, workdir, gpu_available):
-    """RT_TUNE_COLD_ESTIMATE: a new view's first launch is ordered by the primary-walk estimate
-    (k_estimate + the batch sort) instead of screen order; later launches by measured durations.
+    """RT_TUNE_COLD_ESTIMATE: a new view's first launch is ordered centre-out (2, k_estimate_center)
+    or by the primary-walk estimate (1, k_estimate) + the batch sort, instead of screen order (0);
+    later launches by measured durations.
     Every render after RT_TUNE_FORGET_ORDER (cold) and the warm ones after it are byte-identical
     with identical ray counts to screen-order dispatch, with the frame and the shard entry."""
     import torch
@@ -393,7 +395,7 @@ def test_cold_estimate_order_keeps_results(spec, w, h, pf, workdir, gpu_availabl
         fb0 = torch.zeros(h * w * 3, dtype=torch.uint8, device="cuda:0")
         sc.render_frame_device(p, 16, 16, fb0.data_ptr(), fb0.numel(), torch.cuda.current_stream().cuda_stream)
         sc.tune("batch_order", 1)
-        for est in (1, 0, 1):
+        for est in (2, 1, 0, 2):
             sc.tune("cold_estimate", est)
             sc.tune("forget_order", 1)
             for _ in range(3):
@@ -441,7 +443,10 @@ def test_multi_frame_shard_batch_reassembles(workdir, gpu_available):
                                    {"chain_from": 1, "bvh_width": 2}, {"chain_from": 0, "pipes": 1},
                                    {"pipes": 2}, {"pipes": 2, "bvh_grid": 4096}, {"bvh_grid": 65536},
                                    {"fuse_pixels": 0}, {"batch_order": 0}, {"batch_order": 0, "chain_split": 3},
-                                   {"chain_split": 1}, {"chain_split": 2}, {"chain_split": 3}, {"wave_steal": 0},
+                                   {"chain_split": 1}, {"chain_split": 2}, {"chain_split": 3}, {"chain_split": 4},
+                                   {"chain_split": 4, "dyn_group": 0}, {"chain_split": 4, "dyn_group": 6},
+                                   {"chain_split": 4, "wave_steal": 1}, {"chain_split": 4, "bvh_grid": 3},
+                                   {"chain_split": 0}, {"wave_steal": 0},
                                    {"wave_steal": 1}, {"wave_steal": 1, "lds_stack": 1},
                                    {"wave_steal": 1, "bvh_grid": 3}, {"wave_steal": 1, "top_nodes": 0}])
 def test_launch_shape_knobs_never_change_results(knobs, workdir, gpu_available):
@@ -510,15 +515,20 @@ def test_split_batches_match_plain_walk(spec, w, h, pf, pfy, steal, half, quarte
 
 @pytest.mark.parametrize("w,h,pf", [(400, 300, 1), (64, 48, 8), (100, 75, 3)])
 def test_wave_steal_auto_trials_keep_results(w, h, pf, workdir, gpu_available):
-    """RT_TUNE_WAVE_STEAL 2 (default): launches 2 and 3 over a frame geometry are timed without and
-    with stealing, later ones use the faster; every render of the sequence equals the plain walk's
-    (pf 8: 64 sub-samples per pixel, where the half-wave split must stay off)."""
+    """RT_TUNE_WAVE_STEAL 2 with RT_TUNE_CHAIN_SPLIT 5 (the defaults): the first launch over a frame
+    geometry takes its batches dynamically (4), launches 2-5 are the timed trials (steal off/on x
+    block dispatch/dynamic tasks), later ones use the fastest; every render of the sequence equals
+    the plain walk's with block dispatch (pf 8: 64 sub-samples per pixel, where the half-wave split
+    must stay off)."""
     p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=1, lights=[[0, 0, 4]])
     with R.Scene.load(scene_path("ref:dodgeColorTest.obj", workdir), device=0) as sc:
         sc.tune("wave_steal", 0)
+        sc.tune("chain_split", 0)
         ref, reff, refc = sc.render(p, want_f32=True)
         sc.tune("wave_steal", 2)
-        for _ in range(8):
+        sc.tune("chain_split", 5)
+        sc.tune("forget_order", 1)
+        for _ in range(12):
             u8, f32, c = sc.render(p, want_f32=True)
             assert [int(x) for x in c] == [int(x) for x in refc]
             assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
