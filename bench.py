@@ -447,11 +447,12 @@ def main():
             logical = ch_tests / 64.0 * 64.0 + queries * 52.0
         avg_s = ch_ms / 1e3 / max(ch_launches, 1)
         achieved = flops / max(ch_launches, 1) / avg_s / 1e12 if avg_s > 0 else 0.0
-        # the committed PMC summary profiles the default workload (C4): other workloads carry none
+        # the committed PMC summaries: profiles/*_pmc.json profiles the default workload (C4),
+        # profiles/*_pmc_<workload>.json another one (tools/gpu_pmc.sh with WORKLOAD set)
         issue = None
-        if args.workload == "c4" and args.accel == "bvh":
-            traffic, traffic_src = pmc_traffic(kname)
-            pc, pc_src = pmc_counters(kname, "SQ_THREAD_CYCLES_VALU_per_launch")
+        if args.accel == "bvh":
+            traffic, traffic_src = pmc_traffic(kname, args.workload)
+            pc, pc_src = pmc_counters(kname, "SQ_THREAD_CYCLES_VALU_per_launch", args.workload)
             if pc and avg_s > 0 and pc.get("SQ_INSTS_VALU_per_launch") and pc.get("SQ_ACTIVE_INST_VALU_per_launch"):
                 simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
                 iv = pc["SQ_INSTS_VALU_per_launch"]
@@ -591,18 +592,20 @@ def strong_model(t1_ms, crit_ms, shard_ms, frame_bytes, link_gbs=(50.0, 150.0), 
     return out
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*_pmc.json,
-    written by tools/pmc_summary.py from separate rocprofv3 --pmc passes of this bench command)."""
-    c, src = pmc_counters(kernel, "traffic_bytes_per_launch")
+def pmc_traffic(kernel: str, workload: str = "c4"):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary of `workload`
+    (profiles/*_pmc.json for C4, profiles/*_pmc_<workload>.json otherwise; written by
+    tools/pmc_summary.py from separate rocprofv3 --pmc passes of this bench command)."""
+    c, src = pmc_counters(kernel, "traffic_bytes_per_launch", workload)
     return (c["traffic_bytes_per_launch"], src) if c else (None, None)
 
 
-def pmc_counters(kernel: str, need: str):
+def pmc_counters(kernel: str, need: str, workload: str = "c4"):
     """The per-launch counters of `kernel` (its timed instantiation) from the newest committed PMC
-    summary that has counter `need`: (dict, file) or (None, None)."""
+    summary of `workload` that has counter `need`: (dict, file) or (None, None)."""
     import glob
-    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc.json")))   # round-tagged names sort by age
+    suffix = "_pmc.json" if workload == "c4" else f"_pmc_{workload}.json"
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*" + suffix)))   # round-tagged names sort by age
     for f in reversed(files):
         try:
             d = json.load(open(f))

@@ -1,11 +1,12 @@
 #!/bin/bash
 # Build A/B variants of librtamd.so with extra device defines: raytracert_amd/ab/lib_<name>.so.
+# (kernel flags as the Makefile: KFLAGS -fno-slp-vectorize)
 # Usage: tools/build_ab.sh name1 "-DFOO=1 -DBAR=2" name2 "-DFOO=2" ...   (run on the CPU host)
 set -e
 cd "$(dirname "$0")/../raytracert_amd"
 mkdir -p ab build
 rm -f ab/lib_*.so
-HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I../include -Icsrc -Ibuild"
+HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -I../include -Icsrc -Ibuild"
 while [ $# -ge 2 ]; do
   N=$1; D=$2; shift 2
   /opt/rocm/bin/hipcc $HIPFLAGS $D -c csrc/rt_kernels.hip -o ab/k_$N.o &

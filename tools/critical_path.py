@@ -6,6 +6,7 @@ For a workload of bench.py, renders warm frames, takes the per-batch wave lifeti
 of its own chains (walk iterations x load latency); if much faster, it is contention with the rest
 of the frame. Also prints the work counters (rays, node visits, triangle tests) of each rectangle.
 Usage: python tools/critical_path.py [workload] [n_longest]
+RT_CRIT_TUNE='knob=v,knob=v' applies Scene.tune knobs first (e.g. wave_steal=1,split_eighth=512).
 """
 import os
 import sys
@@ -32,6 +33,9 @@ def main():
         p = R.RenderParams(width=wl["width"], height=wl["height"], pf=wl["pf"], max_lvl=wl["max_lvl"],
                            lights=[list(x) for x in wl["lights"]])
         with R.Scene.load(path, device=0) as sc:
+            for kv in filter(None, os.environ.get("RT_CRIT_TUNE", "").split(",")):
+                k, v = kv.split("=")
+                sc.tune(k, int(v))
             for _ in range(8):
                 sc.render(p)
             dur = sc.batch_durations()

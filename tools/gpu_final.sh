@@ -14,6 +14,9 @@ if [ "$2" != "skip-tests" ]; then
 fi
 bash tools/gpu_pmc.sh $TAG > gpurun_out/pmc_$TAG.log 2>&1 || { echo "pmc failed"; tail -20 gpurun_out/pmc_$TAG.log; exit 1; }
 python3 tools/pmc_summary.py gpurun_out/pmc/$TAG gpurun_out/${TAG}_pmc.json > /dev/null && cp gpurun_out/${TAG}_pmc.json profiles/${TAG}_pmc.json
+# the same passes over the 1M-triangle workload (bench --workload c5 reads profiles/*_pmc_c5.json)
+WORKLOAD=c5 bash tools/gpu_pmc.sh ${TAG}_c5 > gpurun_out/pmc_${TAG}_c5.log 2>&1 || { echo "pmc c5 failed"; tail -20 gpurun_out/pmc_${TAG}_c5.log; exit 1; }
+python3 tools/pmc_summary.py gpurun_out/pmc/${TAG}_c5 gpurun_out/${TAG}_pmc_c5.json > /dev/null && cp gpurun_out/${TAG}_pmc_c5.json profiles/${TAG}_pmc_c5.json
 timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "bench failed"; tail -30 gpurun_out/bench_$TAG.err; exit 1; }
 cat gpurun_out/bench_$TAG.json
 # rocprof of the timed entry point: 50 ordered frames dilute the first (unordered) launches; the
