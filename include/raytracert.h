@@ -308,6 +308,14 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
 #define RT_TUNE_DYN_GROUP 29     /* RT_TUNE_CHAIN_SPLIT 4: 2^value consecutive wave tasks (of the batch order)
                                     go to one XCD before the next XCD's turn (default 2: four, as four
                                     consecutive 64-thread waves of a 256-thread block) */
+#define RT_TUNE_SHADOW_HELPERS 30 /* in the split waves of a fused chain launch (RT_TUNE_STEAL_HALF and the
+                                    quarter / eighth tiers, plain kernel) the lanes past the part's
+                                    samples walk shadow rays for their owners: lane o + r x part takes
+                                    lights r, r + roles, ... of sample o, so a sample's lights are walked
+                                    side by side instead of one after another. 1 on, 0 off, 2 (default)
+                                    per view: the launch trials time the plain kernel both ways (C3 0.267
+                                    -> 0.221 ms with, C4 0.416 -> 0.436 ms: its long batches walk more
+                                    closest-hit than shadow nodes). Placement only */
 #define RT_TUNE_TOP_NODES 13     /* retired in r03 (0-85 accepted, no effect): an LDS copy of the four-wide
                                     tree's top levels; with float node rows loaded from global memory it
                                     measured slower (flat loads, 64-bit addresses) */
@@ -361,11 +369,14 @@ int rt_work_detail(rt_scene *scene, int32_t kind, uint64_t out[RT_WORK_FIELDS]);
  * and stamp builds were retired with the variants they measured); 0 in production builds.
  * Reads count words from offset (offset + count <= 131072); synchronises the device. */
 int rt_diag_read(rt_scene *scene, int64_t offset, int64_t count, uint64_t *out);
-/* The per-view launch trials of render pipeline 0 (RT_TUNE_WAVE_STEAL 2 x RT_TUNE_CHAIN_SPLIT 5):
- * info = {trials timed (0 while pending), chosen trial (-1 pending), its wave_steal, its chain
- * distribution}; trial_ms (may be NULL) = each trial's chain-launch time (trial t: steal t % ns,
- * distribution t / ns, ns = 2 when both steal options are tried). Diagnostics; placement only. */
-int rt_scene_trials(rt_scene *scene, int32_t info[4], float trial_ms[4]);
+/* The per-view launch trials of render pipeline 0 (RT_TUNE_WAVE_STEAL 2 x RT_TUNE_CHAIN_SPLIT 5 x
+ * RT_TUNE_SHADOW_HELPERS 2): info = {trials timed (0 while pending), chosen trial (-1 pending), its
+ * wave_steal, its chain distribution, its shadow helpers}; trial_ms (may be NULL) = each trial's
+ * chain-launch time of each candidate. Candidates, per distribution (0, then 4): the plain kernel
+ * (without, then with shadow helpers), then the stealing kernel. After a warm-up launch each is
+ * timed twice (two rounds) and its faster launch counts; the fastest candidate is kept unless within
+ * 2% of candidate 0. Diagnostics; placement only. */
+int rt_scene_trials(rt_scene *scene, int32_t info[5], float trial_ms[8]);
 
 /* Per wave batch of the scene's latest chain launch (pipeline 0): the wave's duration in 100 MHz
  * ticks (s_memrealtime), in batch order (screen order of the batches, not dispatch order). *n_out =

@@ -261,7 +261,8 @@ class Scene:
         """Launch-shape knobs ('xcd_split', 'bvh_grid', 'bvh_width', 'lds_stack', 'pipes',
         'shadow_virtual', 'pipe_batches', 'pipe_priority', 'chain_from', 'chain_split', 'top_nodes',
         'batch_order', 'order_every', 'fuse_pixels', 'wave_steal', 'steal_half', 'steal_quarter',
-        'cold_estimate', 'forget_order', 'split_eighth', 'prio_batches', 'pixel_order', 'dyn_group';
+        'cold_estimate', 'forget_order', 'split_eighth', 'prio_batches', 'pixel_order', 'dyn_group',
+        'shadow_helpers';
         retired, 0 only: 'wave_traversal', 'chain_refill', 'refill_grid'); outputs never depend on
         them."""
         k = {"xcd_split": _capi.TUNE_XCD_SPLIT, "bvh_grid": _capi.TUNE_BVH_GRID,
@@ -277,17 +278,19 @@ class Scene:
              "steal_quarter": _capi.TUNE_STEAL_QUARTER, "cold_estimate": _capi.TUNE_COLD_ESTIMATE,
              "forget_order": _capi.TUNE_FORGET_ORDER, "split_eighth": _capi.TUNE_SPLIT_EIGHTH,
              "prio_batches": _capi.TUNE_PRIORITY_BATCHES,
-             "pixel_order": _capi.TUNE_PIXEL_ORDER, "dyn_group": _capi.TUNE_DYN_GROUP}[knob]
+             "pixel_order": _capi.TUNE_PIXEL_ORDER, "dyn_group": _capi.TUNE_DYN_GROUP,
+             "shadow_helpers": _capi.TUNE_SHADOW_HELPERS}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
 
     def trials(self) -> dict:
-        """rt_scene_trials: the per-view launch trials (steal x distribution) of pipeline 0."""
-        info = np.zeros(4, np.int32)
-        ms = np.zeros(4, np.float32)
+        """rt_scene_trials: the per-view launch trials (steal x distribution x shadow helpers) of
+        pipeline 0."""
+        info = np.zeros(5, np.int32)
+        ms = np.zeros(8, np.float32)
         check(lib().rt_scene_trials(self._h, info.ctypes.data, ms.ctypes.data))
         n = int(info[0])
         return {"trials": n, "choice": int(info[1]), "wave_steal": int(info[2]), "chain_split": int(info[3]),
-                "trial_ms": [round(float(x), 4) for x in ms[:n]]}
+                "shadow_helpers": int(info[4]), "trial_ms": [round(float(x), 4) for x in ms[:n]]}
 
     def batch_durations(self) -> np.ndarray:
         """Per wave batch of the latest chain launch: the wave's duration in microseconds

@@ -91,6 +91,7 @@ struct DevScene {
     int32_t cold_estimate;          // RT_TUNE_COLD_ESTIMATE: 1 primary-walk score, 2 centre-out
     int32_t dyn_group_log2;         // RT_TUNE_DYN_GROUP: log2 of the consecutive wave tasks dealt to one XCD
     int32_t prio_batches;           // RT_TUNE_PRIORITY_BATCHES: longest batches run at raised wave priority
+    int32_t shadow_helpers;         // RT_TUNE_SHADOW_HELPERS: split waves' idle lanes walk their owners' lights
 };
 
 struct DevWork {
@@ -154,6 +155,7 @@ void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t strea
 // (w.batch_cost -> w.batch_order); the next launch over the same batches dispatches in that order
 // (launch_chain(..., ordered = true)). A counting sort: one fill and three small launches.
 constexpr int kOrderBuckets = 128;
+constexpr uint32_t kCostSplit = 0x80000000u;   // batch_cost flag: the batch ran split (lifetime in bits 0-30)
 constexpr int kWaveBatch = 64;   // lanes per wave batch of the chain launch (one sample per lane)
 hipError_t launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream);
 // A cold launch's batch scores (no measured order yet): one primary walk per wave batch of a fused

@@ -442,10 +442,14 @@ __device__ __forceinline__ int32_t node4_next(const Ray4 &R, const Node4Rows &nd
         const float tnz = fmaf(nz[k], inv.z, R.bnz), tfz = fmaf(fz[k], inv.z, R.bfz);
         const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
         const float tx = fminf(fminf(tfx, tfy), tfz);
-        bool h = te <= tx * 1.00001f;
-        if (!kAnyHit) h = h && te <= R.tcull;
-        // te >= 0 (or NaN, then h is false): an integer min keeps a hit child's key below INFINITY
-        tc[k] = h ? __uint_as_float(min(__float_as_uint(te), 0x7f7fffffu)) : INFINITY;
+        // te <= tx (1 + 1e-5) and, closest-hit, te <= tcull, as one compare against their minimum.
+        // te is finite for every non-empty child (bounds and inv are finite and |b inv| < 2^120, so no
+        // FMA overflows; an empty slot's +inf/-inf bounds give te = +inf > tx = -inf), so a wanted
+        // child's key is below INFINITY, which marks the others
+        // (against two compares and an integer min of te: C4 0.418 -> 0.415 ms, C5 6.75 -> 6.71, C3
+        // 0.254 -> 0.247; profiles/r03_ab_node_lim.txt)
+        const float lim = kAnyHit ? tx * 1.00001f : fminf(tx * 1.00001f, R.tcull);
+        tc[k] = te <= lim ? te : INFINITY;
     }
     if (!kAnyHit) {
         // Sorted, branch-free pushes: the wanted children after the first go to the stack with
@@ -1491,17 +1495,29 @@ constexpr int kChainSteps = 256;   // max_lvl <= 254
 // One chain step of one sample (trace, raytracing.cpp:381-406): the closest-hit query, isShadow
 // per light (:241-261), shade (:335-368). Returns the secondary ray (state kChildTrace) or the end
 // of the chain. Shadow-ray statistics are counted per block in s_sh.
+// Shadow helpers (split waves of the fused launch, RT_TUNE_SHADOW_HELPERS): with roles > 1 (wave-
+// uniform) lane o < plen owns a sample and lanes o + r plen (r = 1 .. roles - 1) are its helpers:
+// they take the owner's hit by lane shuffles and walk lights r, r + roles, ... while the owner walks
+// lights 0, roles, ...; the owner ORs their verdicts into its mask and shades. Each light's walk is
+// the same walk on the same ray whichever lane runs it, so the mask is the same bits.
 template <bool kAnyHit, int W, bool kCount, bool kInLane = false, bool kSteal = false>
 __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeParams &p, const DevWork &w, int step,
                                                 int sample, V3 org, V3 dst, int lvl, const LaneStack &stack, int *s_sh,
-                                                WorkTally<kCount> &wc, WorkTally<kCount> &ws) {
+                                                WorkTally<kCount> &wc, WorkTally<kCount> &ws, int role = 0, int roles = 1,
+                                                int plen = kWave) {
     Secondary none;
     none.state = kChildNone;
     none.local = mk(0, 0, 0);   // trace() miss: black (:389-391)
     int bidx = -1;
     V3 bI = mk(0, 0, 0);
-    bvh_query_w<false, W, kSteal>(sc, org, sub(dst, org), true, bidx, bI, stack, wc.tests, wc.visits);
+    bvh_query_w<false, W, kSteal>(sc, org, sub(dst, org), role == 0, bidx, bI, stack, wc.tests, wc.visits);
     if (bidx >= sc.nt) { w.counters[kErrorSlot] = 1; bidx = -1; }
+    const int lane = __lane_id();
+    if (roles > 1) {   // helpers take their owner's hit (owner and helpers are all active here)
+        const int src = role ? lane - role * plen : lane;
+        bidx = __shfl(bidx, src);
+        bI = mk(__shfl(bI.x, src), __shfl(bI.y, src), __shfl(bI.z, src));
+    }
     if (bidx < 0) {
         if (!kInLane) shade_miss(w, step, sample);
         return none;
@@ -1509,16 +1525,21 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
     uint32_t mask = 0;   // isShadow per light (:241-261)
     const bool shadows = (p.flags & RT_SHADOWS) && p.n_lights > 0;
     if (shadows) {
-        atomicAdd(&s_sh[step], p.n_lights);
+        if (role == 0) atomicAdd(&s_sh[step], p.n_lights);
         const V3 so = mk(bI.x + 0.1f, bI.y + 0.1f, bI.z + 0.1f);                // :248
-        for (int l = 0; l < p.n_lights; ++l) {
+        for (int l = role; l < p.n_lights; l += roles) {
             int sidx = -1;
             V3 sI = mk(0, 0, 0);
             const V3 sd = mk(p.lights[l][0] - so.x, p.lights[l][1] - so.y, p.lights[l][2] - so.z);
             bvh_query_w<kAnyHit, W, kSteal>(sc, so, sd, true, sidx, sI, stack, ws.tests, ws.visits);
             if (sidx >= 0 && !sc.mats[sc.tri_mat[sidx]].transparent) mask |= 1u << l;   // :253-257
         }
+        for (int r = 1; r < roles; ++r) {   // the helpers' verdicts (all lanes of the group active again)
+            const uint32_t m = static_cast<uint32_t>(__shfl(static_cast<int>(mask), min(lane + r * plen, kWave - 1)));
+            if (role == 0) mask |= m;
+        }
     }
+    if (role != 0) return none;   // (a helper's return value is not used)
     return shade_hit<kInLane>(sc, p, w, step, sample, sub(dst, org), lvl, bidx, bI, [&](int l) { return ((mask >> l) & 1u) != 0; });
 }
 
@@ -1599,21 +1620,32 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         V3 rgb = mk(0, 0, 0);   // fused pixels: this lane's folded chain and its pixel (valid samples)
         int px = -1;
+        // shadow helpers (RT_TUNE_SHADOW_HELPERS): in a split wave of the fused launch the lanes past
+        // the part's plen samples help their owners' shadow walks, roles = lanes per sample (<= lights)
+        const int roles = (kInLane && !kSteal && nparts > 1 && sc.shadow_helpers && (p.flags & RT_SHADOWS))
+                              ? max(1, min(kWave / plen, p.n_lights)) : 1;
+        const int role = (roles > 1 && lane >= plen && lane < roles * plen) ? lane / plen : 0;
         [&]() {
-        if (!lane_on || j >= nq) return;
-        V3 org, dst;
-        int lvl, sample;
+        bool own = lane_on && j < nq;
+        V3 org = mk(0, 0, 0), dst = mk(0, 0, 0);
+        int lvl = 0, sample = 0;
         if (kInLane) {   // sample j: its primary ray, as k_gen_primary makes it
-            int64_t pxi;
-            int sub;
-            if (!primary_sample(g, j, org, dst, pxi, sub)) {
+            int64_t pxi = 0;
+            int sub = 0;
+            if (own && !primary_sample(g, j, org, dst, pxi, sub)) {
                 if (g.out_mode == 0 && out_u8 && sub == 0) { out_u8[3 * pxi] = 0; out_u8[3 * pxi + 1] = 0; out_u8[3 * pxi + 2] = 0; }
-                return;
+                own = false;
             }
-            px = static_cast<int>(pxi);
+            if (roles > 1) {   // a helper follows its owner's sample (all lanes are still here)
+                const bool o = __shfl(static_cast<int>(own), role ? lane - role * plen : lane) != 0;
+                if (role) own = o;
+            }
+            if (!own || (role == 0 && !lane_on)) return;
+            if (role == 0) px = static_cast<int>(pxi);
             lvl = 0;
             sample = j;
         } else {
+            if (!own) return;
             const float4 qo = w.q_org[first & 1][j], qd = w.q_dst[first & 1][j];
             lvl = as_int(qd.w);
             if (lvl < 0) return;
@@ -1622,9 +1654,15 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
             dst = mk(qd.x, qd.y, qd.z);
         }
         for (int step = first; step < kChainSteps; ++step) {
-            if (step > first) atomicAdd(&s_q[step], 1);
+            if (step > first && role == 0) atomicAdd(&s_q[step], 1);
             const Secondary sec = chain_step<kAnyHit, W, kCount, kInLane, kSteal>(sc, p, w, step, sample, org, dst, lvl, stack,
-                                                                                  s_sh, wc, ws);
+                                                                                  s_sh, wc, ws, role, roles, plen);
+            bool cont = sec.state == kChildTrace;
+            if (roles > 1) cont = __shfl(static_cast<int>(cont), role ? lane - role * plen : lane) != 0;   // the owner's
+            if (role) {
+                if (!cont) break;
+                continue;
+            }
             if (sec.state != kChildTrace) {
                 if (kInLane)   // the chain ends here: fold it in the lane (fold_chain's arithmetic)
                     rgb = fold_inlane(sc, w, first, step, sample,
@@ -1644,8 +1682,14 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
             acc = mk(acc.x / div, acc.y / div, acc.z / div);   // operator/, Vec3D.h:36-38
             if (lane == pix_lane && px >= 0) store_pixel(acc, 3 * static_cast<int64_t>(px), out_u8, out_f32);
         }
-        if (lane == 0 && wave_on)   // (a split batch: its parts' lifetimes, the last to finish stored)
-            w.batch_cost[pb] = static_cast<uint32_t>(min(__builtin_amdgcn_s_memrealtime() - t0, 0xFFFFFFFFull));
+        // the batch's lifetime (a split batch: its parts' lifetimes, the last to finish stored), with
+        // bit 31 set for a split batch (kCostSplit): the sort counts it double, so a batch that ran
+        // faster because it was split (or helped) stays at the head of the order instead of
+        // dropping out of the split tier and back in on every re-sort
+        if (lane == 0 && wave_on) {
+            const uint32_t d = static_cast<uint32_t>(min(__builtin_amdgcn_s_memrealtime() - t0, 0x7FFFFFFFull));
+            w.batch_cost[pb] = nparts > 1 ? (d | kCostSplit) : d;
+        }
     }, dyn ? sc.dyn_group_log2 : 0);
     wc.flush(sc.work);
     ws.flush(sc.work ? sc.work + kWorkFields : nullptr);
@@ -1752,6 +1796,7 @@ __global__ __launch_bounds__(kBlock) void k_fold_rays(DevWork w, int32_t n, floa
 // unequal costs leave XCDs idle. DESIGN.md §7.)
 constexpr int kOrderBlock = 256;
 __device__ __forceinline__ int order_bucket(uint32_t c) {
+    if (c & kCostSplit) c = min((c & ~kCostSplit) * 2u, ~kCostSplit);   // a split batch counts double
     if (c < 4) return kOrderBuckets - 1;
     const int e = 31 - __clz(c);
     const int k = 4 * e + static_cast<int>((c >> (e - 2)) & 3u);

@@ -513,14 +513,42 @@ def test_split_batches_match_plain_walk(spec, w, h, pf, pfy, steal, half, quarte
             assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
 
 
+@pytest.mark.parametrize("spec,w,h,pf,lights,half,quarter,eighth", [
+    ("syn:C4", 240, 135, 1, 2, 512, 0, 0), ("syn:C4", 240, 135, 1, 4, 64, 64, 64), ("syn:F4", 96, 54, 2, 3, 512, 8, 8),
+    ("ref:dodgeColorTest.obj", 200, 150, 1, 1, 512, 0, 0), ("syn:F4", 60, 34, 3, 2, 512, 8, 8),
+    ("syn:C4", 160, 90, 1, 16, 32, 32, 32)])
+def test_shadow_helpers_match_plain_walk(spec, w, h, pf, lights, half, quarter, eighth, workdir, gpu_available):
+    """RT_TUNE_SHADOW_HELPERS: in split waves (half, quarter, eighth tiers of ordered launches) the
+    lanes past a part's samples walk some of their owners' lights; with 1 to 16 lights (1: no helper
+    roles), pf 1-3 (pf 3: a 36-lane half leaves no whole helper group), transparency (closest-hit
+    shadows, F4). Frames, floats and ray counts equal the unsplit plain walk's on every launch."""
+    L = [[0, 0, 4], [1.5, 1.5, 4], [-1.5, 1.5, 4], [0, -1.5, 4]] * 4
+    p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=3, lights=L[:lights])
+    with R.Scene.load(scene_path(spec, workdir), device=0) as sc:
+        sc.tune("wave_steal", 0)
+        sc.tune("chain_split", 0)
+        sc.tune("steal_half", 0)
+        ref, reff, refc = sc.render(p, want_f32=True)
+        sc.tune("steal_half", half)
+        sc.tune("steal_quarter", quarter)
+        sc.tune("split_eighth", eighth)
+        for i in range(5):
+            sc.tune("shadow_helpers", 0 if i == 2 else 1)
+            u8, f32, c = sc.render(p, want_f32=True)
+            assert [int(x) for x in c] == [int(x) for x in refc]
+            assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
+
+
 @pytest.mark.parametrize("w,h,pf", [(400, 300, 1), (64, 48, 8), (100, 75, 3)])
 def test_wave_steal_auto_trials_keep_results(w, h, pf, workdir, gpu_available):
-    """RT_TUNE_WAVE_STEAL 2 with RT_TUNE_CHAIN_SPLIT 5 (the defaults): the first launch over a frame
-    geometry takes its batches dynamically (4), launches 2-5 are the timed trials (steal off/on x
-    block dispatch/dynamic tasks), later ones use the fastest; every render of the sequence equals
-    the plain walk's with block dispatch (pf 8: 64 sub-samples per pixel, where the half-wave split
-    must stay off)."""
-    p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=1, lights=[[0, 0, 4]])
+    """RT_TUNE_WAVE_STEAL 2 with RT_TUNE_CHAIN_SPLIT 5 and RT_TUNE_SHADOW_HELPERS 2 (the defaults):
+    the first launch over a frame geometry takes its batches dynamically (4), the next re-sort the
+    order each time until it was measured under a measured order, then 13 launches are the
+    timed trials (a warm-up, then two rounds over the six candidates: per distribution, plain without
+    and with shadow helpers, stealing), later ones use
+    the fastest; every render of the sequence equals the plain walk's with block dispatch (pf 8: 64
+    sub-samples per pixel, where the half-wave split must stay off), and the trials are reported."""
+    p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=1, lights=[[0, 0, 4], [1.5, 1.5, 4]])
     with R.Scene.load(scene_path("ref:dodgeColorTest.obj", workdir), device=0) as sc:
         sc.tune("wave_steal", 0)
         sc.tune("chain_split", 0)
@@ -528,10 +556,13 @@ def test_wave_steal_auto_trials_keep_results(w, h, pf, workdir, gpu_available):
         sc.tune("wave_steal", 2)
         sc.tune("chain_split", 5)
         sc.tune("forget_order", 1)
-        for _ in range(12):
+        for _ in range(22):
             u8, f32, c = sc.render(p, want_f32=True)
             assert [int(x) for x in c] == [int(x) for x in refc]
             assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
+        t = sc.trials()
+        assert t["trials"] == 6 and 0 <= t["choice"] < 6 and len(t["trial_ms"]) == 6
+        assert t["wave_steal"] in (0, 1) and t["chain_split"] in (0, 4) and t["shadow_helpers"] in (0, 1)
 
 
 @pytest.mark.parametrize("spec,w,h,pf,pfy,flags", [("syn:C4", 333, 187, 3, 3, 0), ("syn:F4", 96, 54, 3, 3, 0),
