@@ -87,7 +87,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)   # ~50 ms of C4 frames: fixed sync costs amortised
-    ap.add_argument("--warmup", type=int, default=30)   # covers the batch order's first re-sorts and the launch trials (13 launches)
+    ap.add_argument("--warmup", type=int, default=30)   # covers the batch order's first re-sorts and the launch trials (9 launches)
     ap.add_argument("--mode", choices=("weak", "strong"), default="weak")
     ap.add_argument("--cpu-sample-every", type=int, default=0,
                     help="CPU baseline: every k-th tile (0: the workload's default, C2 the full frame)")

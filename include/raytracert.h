@@ -312,10 +312,9 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
                                     quarter / eighth tiers, plain kernel) the lanes past the part's
                                     samples walk shadow rays for their owners: lane o + r x part takes
                                     lights r, r + roles, ... of sample o, so a sample's lights are walked
-                                    side by side instead of one after another. 1 on, 0 off, 2 (default)
-                                    per view: the launch trials time the plain kernel both ways (C3 0.267
-                                    -> 0.221 ms with, C4 0.416 -> 0.436 ms: its long batches walk more
-                                    closest-hit than shadow nodes). Placement only */
+                                    side by side instead of one after another. 1 (default) on, 0 off,
+                                    2 per view: the launch trials time the plain kernel both ways. C3
+                                    0.263 -> 0.212 ms, C4 0.412 -> 0.397 ms, C5 equal. Placement only */
 #define RT_TUNE_TOP_NODES 13     /* retired in r03 (0-85 accepted, no effect): an LDS copy of the four-wide
                                     tree's top levels; with float node rows loaded from global memory it
                                     measured slower (flat loads, 64-bit addresses) */

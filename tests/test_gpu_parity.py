@@ -516,7 +516,8 @@ def test_split_batches_match_plain_walk(spec, w, h, pf, pfy, steal, half, quarte
 @pytest.mark.parametrize("spec,w,h,pf,lights,half,quarter,eighth", [
     ("syn:C4", 240, 135, 1, 2, 512, 0, 0), ("syn:C4", 240, 135, 1, 4, 64, 64, 64), ("syn:F4", 96, 54, 2, 3, 512, 8, 8),
     ("ref:dodgeColorTest.obj", 200, 150, 1, 1, 512, 0, 0), ("syn:F4", 60, 34, 3, 2, 512, 8, 8),
-    ("syn:C4", 160, 90, 1, 16, 32, 32, 32)])
+    ("syn:C4", 160, 90, 1, 16, 32, 32, 32), ("ref:dodgeColorTest.obj", 400, 300, 1, 2, 512, 0, 0),
+    ("syn:C4", 480, 270, 1, 2, 4096, 0, 0)])
 def test_shadow_helpers_match_plain_walk(spec, w, h, pf, lights, half, quarter, eighth, workdir, gpu_available):
     """RT_TUNE_SHADOW_HELPERS: in split waves (half, quarter, eighth tiers of ordered launches) the
     lanes past a part's samples walk some of their owners' lights; with 1 to 16 lights (1: no helper
@@ -541,7 +542,7 @@ def test_shadow_helpers_match_plain_walk(spec, w, h, pf, lights, half, quarter, 
 
 @pytest.mark.parametrize("w,h,pf", [(400, 300, 1), (64, 48, 8), (100, 75, 3)])
 def test_wave_steal_auto_trials_keep_results(w, h, pf, workdir, gpu_available):
-    """RT_TUNE_WAVE_STEAL 2 with RT_TUNE_CHAIN_SPLIT 5 and RT_TUNE_SHADOW_HELPERS 2 (the defaults):
+    """RT_TUNE_WAVE_STEAL 2 with RT_TUNE_CHAIN_SPLIT 5 (the defaults) and RT_TUNE_SHADOW_HELPERS 2:
     the first launch over a frame geometry takes its batches dynamically (4), the next re-sort the
     order each time until it was measured under a measured order, then 13 launches are the
     timed trials (a warm-up, then two rounds over the six candidates: per distribution, plain without
@@ -555,6 +556,7 @@ def test_wave_steal_auto_trials_keep_results(w, h, pf, workdir, gpu_available):
         ref, reff, refc = sc.render(p, want_f32=True)
         sc.tune("wave_steal", 2)
         sc.tune("chain_split", 5)
+        sc.tune("shadow_helpers", 2)
         sc.tune("forget_order", 1)
         for _ in range(22):
             u8, f32, c = sc.render(p, want_f32=True)

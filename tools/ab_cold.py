@@ -19,7 +19,7 @@ import raytracert_amd as R  # noqa: E402
 # the library's defaults, restored after each variant (rt_capi.cpp rt_scene)
 KNOB_DEFAULTS = {"cold_estimate": 2, "bvh_grid": 16384, "chain_split": 5, "dyn_group": 2, "wave_steal": 2,
                  "pixel_order": 2, "steal_half": 512, "steal_quarter": 0, "split_eighth": 0, "prio_batches": 0,
-                 "order_every": 8, "batch_order": 1, "shadow_helpers": 2}
+                 "order_every": 8, "batch_order": 1, "shadow_helpers": 1}
 wl_name = sys.argv[1] if len(sys.argv) > 1 else "c4"
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 variants = [dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in v.split(",") if kv) for v in (sys.argv[3:] or [""])]
