@@ -315,6 +315,12 @@ int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
                                     side by side instead of one after another. 1 (default) on, 0 off,
                                     2 per view: the launch trials time the plain kernel both ways. C3
                                     0.263 -> 0.212 ms, C4 0.412 -> 0.397 ms, C5 equal. Placement only */
+#define RT_TUNE_FRAMES_IN_FLIGHT 31 /* 1-4 (default 1): calls that render on one pipeline (the default)
+                                    rotate over this many pipelines (workspace, batch order, trials), so
+                                    a caller that queues consecutive frames on as many alternating
+                                    streams keeps that many frames in flight: a frame's launch starts as
+                                    the previous frame's short batches retire, beside its longest
+                                    ones. Calls on one stream stay serialised. Placement only */
 #define RT_TUNE_TOP_NODES 13     /* retired in r03 (0-85 accepted, no effect): an LDS copy of the four-wide
                                     tree's top levels; with float node rows loaded from global memory it
                                     measured slower (flat loads, 64-bit addresses) */

@@ -43,6 +43,7 @@ TUNE_COLD_ESTIMATE, TUNE_FORGET_ORDER = 24, 25
 TUNE_STEAL_HALF, TUNE_STEAL_QUARTER = 22, 23
 TUNE_SPLIT_EIGHTH, TUNE_PRIORITY_BATCHES, TUNE_PIXEL_ORDER, TUNE_DYN_GROUP = 26, 27, 28, 29
 TUNE_SHADOW_HELPERS = 30
+TUNE_FRAMES_IN_FLIGHT = 31
 BVH_INFO_FIELDS = 7
 STOCHASTIC = 1 << 8
 DEFAULT_SEED = 0x5EED

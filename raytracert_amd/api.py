@@ -262,7 +262,7 @@ class Scene:
         'shadow_virtual', 'pipe_batches', 'pipe_priority', 'chain_from', 'chain_split', 'top_nodes',
         'batch_order', 'order_every', 'fuse_pixels', 'wave_steal', 'steal_half', 'steal_quarter',
         'cold_estimate', 'forget_order', 'split_eighth', 'prio_batches', 'pixel_order', 'dyn_group',
-        'shadow_helpers';
+        'shadow_helpers', 'frames_in_flight';
         retired, 0 only: 'wave_traversal', 'chain_refill', 'refill_grid'); outputs never depend on
         them."""
         k = {"xcd_split": _capi.TUNE_XCD_SPLIT, "bvh_grid": _capi.TUNE_BVH_GRID,
@@ -279,7 +279,7 @@ class Scene:
              "forget_order": _capi.TUNE_FORGET_ORDER, "split_eighth": _capi.TUNE_SPLIT_EIGHTH,
              "prio_batches": _capi.TUNE_PRIORITY_BATCHES,
              "pixel_order": _capi.TUNE_PIXEL_ORDER, "dyn_group": _capi.TUNE_DYN_GROUP,
-             "shadow_helpers": _capi.TUNE_SHADOW_HELPERS}[knob]
+             "shadow_helpers": _capi.TUNE_SHADOW_HELPERS, "frames_in_flight": _capi.TUNE_FRAMES_IN_FLIGHT}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
 
     def trials(self) -> dict:
