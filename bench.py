@@ -112,6 +112,9 @@ def parse():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c4")
     ap.add_argument("--no-bf-roofline", action="store_true", help="skip the brute-force kernel's roofline frame")
     ap.add_argument("--pipes", type=int, default=1, help="render pipelines a call's batches overlap on")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="N=1 frame path: frames in flight (RT_TUNE_FRAMES_IN_FLIGHT), consecutive frames "
+                         "on this many alternating streams into their own buffers")
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
                     help="extra launch-shape knob (Scene.tune), e.g. shadow_virtual=-1; repeatable")
     return ap.parse_args()
@@ -203,11 +206,15 @@ def main():
             self.bufs = [torch.zeros(self.plan.shard_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
             self.index = torch.as_tensor(self.plan.gather_index(), device=dev)
             if frame_path:
-                self.fbufs = [torch.zeros(HEIGHT * WIDTH * 3, dtype=torch.uint8, device=dev) for _ in range(2)]
+                self.fbufs = [torch.zeros(HEIGHT * WIDTH * 3, dtype=torch.uint8, device=dev)
+                              for _ in range(max(2, args.inflight))]
+                # frames in flight: frame i on stream i % F (the first is the bench's stream)
+                self.fstreams = [stream] + [torch.cuda.Stream(dev) for _ in range(max(args.inflight, 1) - 1)]
             elif rank == 0:
                 self.frames_out = [torch.zeros(frames * HEIGHT * WIDTH * 3, dtype=torch.uint8, device=dev) for _ in range(2)]
             else:
                 self.frames_out = [torch.zeros(1, dtype=torch.uint8, device=dev)] * 2
+            self.fif = 1   # frames in flight of the current run (the timed run sets args.inflight)
             self.nfin = 0
             self.pending = []
             # rank 0 un-permutes on a side stream, so the next step's render is not queued behind it
@@ -224,8 +231,9 @@ def main():
         def render_once(self, i=0):
             """The step's render call alone (the roofline's profiled launches use this)."""
             if self.single:
-                fb = self.fbufs[i % 2]
-                scene.render_frame_device(cparams, TILE, TILE, fb.data_ptr(), fb.numel(), stream.cuda_stream)
+                fb = self.fbufs[i % max(2, self.fif)]
+                st = self.fstreams[i % self.fif]
+                scene.render_frame_device(cparams, TILE, TILE, fb.data_ptr(), fb.numel(), st.cuda_stream)
                 return fb
             return self.render_shard(buf=self.bufs[i % 2])
 
@@ -309,7 +317,23 @@ def main():
     rays_by_kind = [int(x) for x in ct.tolist()]
 
     # ---- timed region (the metric) ----
-    elapsed, frames = main_run.run(args.steps, args.warmup)
+    inflight = max(1, args.inflight) if main_run.single else 1
+    if inflight > 1:
+        # one frame at a time first: pipeline 0 learns the batch order and decides the launch trials
+        # with no other frame beside its launches; the other pipelines then learn their orders and
+        # adopt that decision
+        main_run.run(0, args.warmup)
+        scene.tune("frames_in_flight", inflight)
+        main_run.fif = inflight
+    elapsed, frames = main_run.run(args.steps, args.warmup * inflight)
+    one_in_flight = None
+    if inflight > 1:   # the same frames one at a time (each frame's own latency, back to back)
+        scene.tune("frames_in_flight", 1)
+        main_run.fif = 1
+        el1, _ = main_run.run(args.steps, args.warmup)
+        one_in_flight = {"ms_per_step": round(el1 / args.steps * 1e3, 3),
+                         "value": round(rays_per_step * args.steps / el1 / 1e6, 4),
+                         "what": "the same timed loop with one frame in flight (each launch waits for the previous frame)"}
 
     rehearsal = None
     if args.rehearse and rank == 0 and frames is not None:   # every assembled frame = the one-GPU frame
@@ -499,6 +523,12 @@ def main():
                 "rays_per_step": int(rays_per_step),
                 "rays_by_kind_per_step": {"primary": rays_by_kind[0], "secondary": rays_by_kind[1], "shadow": rays_by_kind[2]},
                 "frame_ms_per_gpu": round(elapsed / args.steps * 1e3, 3),
+                "frames_in_flight": inflight,
+                "frames_in_flight_what": "consecutive frames of the view on alternating streams, each into its own "
+                                         "buffer and fully rendered (RT_TUNE_FRAMES_IN_FLIGHT): a frame's launch starts "
+                                         "while the previous frame's longest batches still run; ms_per_step is then "
+                                         "the per-frame throughput time, one_in_flight the frame-after-frame time",
+                "one_in_flight": one_in_flight,
                 "first_frame_ms": round(cold_ms, 3) if cold_ms is not None else None,
                 "first_frame_what": "a new view's first frame (no measured batch order or launch trial: every order "
                                     "forgotten first), dispatched centre-out (RT_TUNE_COLD_ESTIMATE 2) as dynamic "
