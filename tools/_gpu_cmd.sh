@@ -1,5 +1,6 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu_r03h.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pytest_gpu_r03h.log; exit 1; }
-tail -1 gpurun_out/pytest_gpu_r03h.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" 2>&1 | tail -2
+timeout -k 10 300 python tools/ab_cold.py ref_default 6 "" "steal_quarter=64" 2>&1 | grep -v amdgpu.ids | tee gpurun_out/ab_q2.txt || exit 1
+timeout -k 10 300 python tools/ab_cold.py c4 4 "" "steal_quarter=64" 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/ab_q2.txt || exit 1
+timeout -k 10 300 python tools/ab_cold.py c2 4 "" "steal_quarter=64" 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/ab_q2.txt || exit 1
+timeout -k 10 300 python tools/ab_cold.py c3 4 "" "steal_quarter=64" 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/ab_q2.txt || exit 1
