@@ -47,7 +47,11 @@ extern "C" {
 #define RT_E_NODEV  -6   /* no usable gfx950 device */
 #define RT_E_RCCL   -7   /* an RCCL call failed, or the communicator reported an asynchronous error */
 
+/* Lights held inline in rt_params (the reference's MyLightPositions is an unbounded std::vector,
+ * raytracing.h:9, grown by the 'L' key, main.cpp:334-336): up to RT_MAX_LIGHTS in lights[][], any
+ * number (up to RT_LIGHTS_LIMIT) through rt_params.light_list. */
 #define RT_MAX_LIGHTS 16
+#define RT_LIGHTS_LIMIT 65536
 
 /* Feature switches (raytracing.cpp:15-20; keyboard keys 1-6, raytracing.cpp:456-473). */
 #define RT_AMBIENT    (1u << 0)
@@ -93,11 +97,15 @@ typedef struct {
     int32_t pfx, pfy;             /* pixelfactorX / pixelfactorY (raytracing.cpp:23-25), >= 1 */
     int32_t max_lvl;              /* max recursion level (raytracing.cpp:29), >= 0 */
     uint32_t flags;               /* RT_AMBIENT ... RT_REFRACTION */
-    int32_t n_lights;             /* MyLightPositions.size(), 0..RT_MAX_LIGHTS */
+    int32_t n_lights;             /* MyLightPositions.size(): 0..RT_MAX_LIGHTS, or 0..RT_LIGHTS_LIMIT with light_list */
     int32_t seed;                 /* RT_STOCHASTIC only (else ignored): jitter hash seed */
     float lights[RT_MAX_LIGHTS][3];
     float camera_pos[3];          /* MyCameraPosition (raytracing.h:10) */
     float corners[8][3];          /* origin00,dest00, origin01,dest01, origin10,dest10, origin11,dest11 */
+    /* NULL: the lights are lights[0..n_lights). Else n_lights x 3 floats (host memory, read during the
+     * call; a std::vector<Vec3Df>'s data() is such an array) and lights[][] is ignored: any number of
+     * lights, shaded in order as shade() loops over MyLightPositions (raytracing.cpp:342). */
+    const float *light_list;
 } rt_params;
 
 typedef struct rt_scene rt_scene;
@@ -176,6 +184,23 @@ int rt_render_tile(rt_scene *scene, const rt_params *params, int32_t x0, int32_t
  * later work queued on it sees the finished tiles (the renderer forks its pipelines from it and
  * joins them back). The call returns after enqueueing (no host synchronisation) unless
  * counts != NULL. Returns the number of tiles written via n_tiles_out. */
+/* Every sub-sample of the 'r' loop (main.cpp:369-388) for the frame params describes, in the loop's call
+ * order: record k = ((y * width + x) * pfx + subx) * pfy + suby holds performRayTracing(origin, dest) of the
+ * loop's ray for (x, y, subx, suby), unclamped (raytracing.cpp:410-416). layout RT_SAMPLES_RGB: 3 floats
+ * per record, the colour; RT_SAMPLES_RAY_RGB: 9 floats, the ray's origin and dest as the device made them
+ * (the loop's binary32 expressions, main.cpp:380-386), then the colour. A host that runs the loop unchanged
+ * can answer each call from here once it finds the call's ray equal to the record's, bit for bit
+ * (include/raytracert_dropin.hpp does). out is host memory of `capacity` floats (>= layout x width x height
+ * x pfx x pfy, below 2^31 records); pinned memory from rt_host_alloc copies fastest. counts as
+ * rt_render_tile. */
+#define RT_SAMPLES_RGB     3
+#define RT_SAMPLES_RAY_RGB 9
+int rt_trace_frame_samples(rt_scene *scene, const rt_params *params, int32_t layout, float *out, size_t capacity,
+                           uint64_t counts[3]);
+/* Page-locked host memory (hipHostMalloc on the scene's device's runtime), for rt_trace_frame_samples'
+ * output and other large device-to-host results. */
+int  rt_host_alloc(size_t bytes, void **out);
+void rt_host_free(void *ptr);
 /* The whole frame, row-major (height x width x 3 bytes, the PPM's pixel order), into the DEVICE
  * buffer d_out_u8, rendered in tile_w x tile_h tiles; stream semantics as rt_render_tiles_device.
  * The single-GPU form of the shard + gather path (no un-permute needed). */
@@ -244,102 +269,6 @@ int rt_scene_bvh_validate(rt_scene *scene);
  * Returns 0 (box written), 1 (ill-conditioned: tested by every query) or 2 (never accepted). */
 int rt_bvh_acceptance_box(const float T[9], float lo[3], float hi[3]);
 
-/* ---- tuning (launch-shape knobs; results never depend on them) ------------------------- */
-#define RT_TUNE_XCD_SPLIT 0   /* BVH queue distribution: 0 grid-stride, 1 one static segment per XCD,
-                                 2 per-XCD segments with work-stealing wave counters */
-#define RT_TUNE_BVH_GRID  1   /* grid cap (blocks of 256 threads) of the BVH kernels; default 16384: the
-                                 chain launch then gives each wave one 64-sample batch of a C4 frame
-                                 and the dispatcher balances the blocks */
-#define RT_TUNE_BVH_WIDTH 2   /* 4 (default): quantised four-wide nodes; 2: float binary nodes */
-#define RT_TUNE_LDS_STACK 3   /* traversal stack entries per lane kept in LDS; deeper ones in HBM */
-#define RT_TUNE_PIPES     4   /* 1-4 render pipelines (workspace + stream) a call's batches overlap on
-                                 (default 1) */
-#define RT_TUNE_WAVE_TRAVERSAL 8   /* retired in r03 (only 0 accepted): the wave-coherent walk of the
-                                      four-wide tree measured no faster on C4, primaries included */
-#define RT_TUNE_CHAIN_FROM 9     /* chain steps from this one on run in one launch, each lane carrying
-                                    its ray through closest-hit, shadows and shade (default 0;
-                                    >= max_lvl + 1: every step its own launches) */
-#define RT_TUNE_BATCH_ORDER 15  /* 1 (default): the chain launch dispatches its wave batches longest
-                                    first, by the durations the pipeline's previous launch over the
-                                    same batches measured (the first launch runs in screen order);
-                                    0: screen order */
-#define RT_TUNE_ORDER_EVERY 17  /* batch order re-sorted every this many launches over the same batches
-                                    (default 8; 1: every launch); the durations are measured every time */
-#define RT_TUNE_FUSE_PIXELS 18  /* 1 (default): the chain launch writes each pixel when its samples'
-                                    chains end (no separate frame pass) when pfx*pfy <= 64 (a wave
-                                    batch holds floor(64 / spp) whole pixels); 0: always the frame pass */
-#define RT_TUNE_CHAIN_REFILL 19  /* retired in r03 (only 0 accepted): per-lane pixel refill measured 1.5x
-                                    slower on C4 (a wave's rays lose their shared chain step) */
-#define RT_TUNE_REFILL_GRID 20   /* retired in r03 with it (only 0 accepted) */
-#define RT_TUNE_WAVE_STEAL 21    /* in-wave work stealing in the chain launch: a lane whose query is done
-                                    walks a subtree from another lane's stack with that lane's ray
-                                    (four-wide tree). 0 off, 1 on, 2 (default, auto): the second and
-                                    third launches over a frame geometry are timed without and with it
-                                    and later ones use the faster (before that: on when the launch is at
-                                    most two rounds of resident waves). C2 0.24 -> 0.18 ms, C3 -4%;
-                                    C4 is faster without */
-#define RT_TUNE_STEAL_HALF 22    /* ordered chain launches: at most this many of the longest batches (and at
-                                    most 1/32 of all, with the quarter and eighth tiers) run as two waves
-                                    of half the batch's pixels each, so the longest chains of a frame use
-                                    more SIMDs at once; in the stealing kernel the idle lanes of each start
-                                    as helpers (default 512; 0 off; needs >= 2 pixels per batch) */
-#define RT_TUNE_COLD_ESTIMATE 24 /* how a fused launch over batches with no measured order (a new view's
-                                    first frame) is ordered: 2 (default) centre-out, by the distance of
-                                    each batch from the frame's centre (no walk); 1 a pre-pass that walks
-                                    one primary ray per wave batch and scores the batch; 0 screen order.
-                                    C4 cold frame 0.62 / 0.70 / 0.63 ms, C2 0.20 / 0.23 / 0.23 */
-#define RT_TUNE_FORGET_ORDER 25  /* any value: drop every measured batch order and wave-steal trial, so the
-                                    next launch runs as a new view's first frame (benchmarks, tests) */
-#define RT_TUNE_STEAL_QUARTER 23 /* ... and before them this many of the longest run as four waves of a
-                                    quarter of the pixels each (default 0; needs >= 4 pixels per batch) */
-#define RT_TUNE_SPLIT_EIGHTH 26  /* ... and before those this many as eight waves of an eighth of the pixels
-                                    (default 0; needs >= 8 pixels per batch) */
-#define RT_TUNE_PRIORITY_BATCHES 27 /* ordered chain launches: the waves of this many of the longest batches
-                                    (with their split parts) run at raised wave priority, so their
-                                    SIMDs issue them first (the longest batch is the frame's critical
-                                    path); default 0 */
-#define RT_TUNE_PIXEL_ORDER 28   /* which pixels of a tile share a wave batch (samples are tile-major):
-                                    0 row-major (a 64-sample batch of a 16x16 tile is 16x4 pixels),
-                                    1 Morton order in square power-of-two tiles (8x8 pixels at pf 1,
-                                    4x4 at pf 2: the rays of a batch stay closer together), 2 (default)
-                                    Morton when pfx*pfy is a power of two and the launch is not one the
-                                    stealing kernel may take (at most two rounds of resident waves),
-                                    else row-major. C4 0.465 -> 0.430 ms, C5 8.47 -> 7.09 ms */
-#define RT_TUNE_DYN_GROUP 29     /* RT_TUNE_CHAIN_SPLIT 4: 2^value consecutive wave tasks (of the batch order)
-                                    go to one XCD before the next XCD's turn (default 2: four, as four
-                                    consecutive 64-thread waves of a 256-thread block) */
-#define RT_TUNE_SHADOW_HELPERS 30 /* in the split waves of a fused chain launch (RT_TUNE_STEAL_HALF and the
-                                    quarter / eighth tiers, plain kernel) the lanes past the part's
-                                    samples walk shadow rays for their owners: lane o + r x part takes
-                                    lights r, r + roles, ... of sample o, so a sample's lights are walked
-                                    side by side instead of one after another. 1 (default) on, 0 off,
-                                    2 per view: the launch trials time the plain kernel both ways. C3
-                                    0.263 -> 0.212 ms, C4 0.412 -> 0.397 ms, C5 equal. Placement only */
-#define RT_TUNE_FRAMES_IN_FLIGHT 31 /* 1-4 (default 1): calls that render on one pipeline (the default)
-                                    rotate over this many pipelines (workspace, batch order, trials), so
-                                    a caller that queues consecutive frames on as many alternating
-                                    streams keeps that many frames in flight: a frame's launch starts as
-                                    the previous frame's short batches retire, beside its longest
-                                    ones. Calls on one stream stay serialised. Placement only */
-#define RT_TUNE_TOP_NODES 13     /* retired in r03 (0-85 accepted, no effect): an LDS copy of the four-wide
-                                    tree's top levels; with float node rows loaded from global memory it
-                                    measured slower (flat loads, 64-bit addresses) */
-#define RT_TUNE_CHAIN_SPLIT 12   /* query distribution of the chain launch: as RT_TUNE_XCD_SPLIT, or 3: 64-query
-                                    chunks dealt round-robin to the XCDs and taken dynamically within
-                                    each, or 4 (fused frame launches; others use 0): a resident grid
-                                    whose waves each take a first wave batch by position and later ones
-                                    from per-XCD counters (RT_TUNE_DYN_GROUP consecutive batches per
-                                    XCD), in batch order once one is measured, so no wave slot waits for
-                                    the rest of its block to retire; 5 (default, auto): 4 for a cold
-                                    launch, then the per-view trials (RT_TUNE_WAVE_STEAL) also time 0
-                                    against 4 and keep the faster (rt_scene_trials) */
-#define RT_TUNE_PIPE_BATCHES 6     /* split a call into at least pipes x this many batches */
-#define RT_TUNE_PIPE_PRIORITY 7    /* 1 (default): pipelines after the first run at lower stream priority */
-#define RT_TUNE_SHADOW_VIRTUAL 5   /* bit k: step k's shadow rays are read from its hits directly
-                                      (no compacted shadow queue); default 1: step 0, whose
-                                      queue is dense and mostly hits */
-int rt_scene_tune(rt_scene *scene, int32_t knob, int32_t value);
-
 /* ---- measurement ---------------------------------------------------------------------- */
 /* Kernel kinds for rt_kernel_stats. */
 #define RT_KERNEL_CLOSEST_HIT 0   /* closest-hit over all triangles (primary + secondary queries) */
@@ -365,37 +294,9 @@ int rt_reset_stats(rt_scene *scene);
  * (RT_KERNEL_CLOSEST_HIT or RT_KERNEL_SHADOW) while profiling was RT_PROFILE_WORK, since the last
  * reset (synchronises the device). */
 int rt_work_stats(rt_scene *scene, int32_t kind, double *tests, double *node_visits);
-/* The same counters in full: [0] tests, [1] node visits, [2] sum over wave tasks (64 queries side
- * by side) of the largest per-query visit count, [3] largest visit count of any query, [4] wave
- * tasks, [5] sum over wave tasks of the largest per-query test count. */
-#define RT_WORK_FIELDS 6
-int rt_work_detail(rt_scene *scene, int32_t kind, uint64_t out[RT_WORK_FIELDS]);
-/* Diagnostic words reserved for diagnostic kernel builds (none in r03: the wave-time, region-count
- * and stamp builds were retired with the variants they measured); 0 in production builds.
- * Reads count words from offset (offset + count <= 131072); synchronises the device. */
-int rt_diag_read(rt_scene *scene, int64_t offset, int64_t count, uint64_t *out);
-/* The per-view launch trials of render pipeline 0 (RT_TUNE_WAVE_STEAL 2 x RT_TUNE_CHAIN_SPLIT 5 x
- * RT_TUNE_SHADOW_HELPERS 2): info = {trials timed (0 while pending), chosen trial (-1 pending), its
- * wave_steal, its chain distribution, its shadow helpers}; trial_ms (may be NULL) = each trial's
- * chain-launch time of each candidate. Candidates, per distribution (0, then 4): the plain kernel
- * (without, then with shadow helpers), then the stealing kernel. After a warm-up launch each is
- * timed twice (two rounds) and its faster launch counts; the fastest candidate is kept unless within
- * 2% of candidate 0. Diagnostics; placement only. */
-int rt_scene_trials(rt_scene *scene, int32_t info[5], float trial_ms[8]);
-
-/* Per wave batch of the scene's latest chain launch (pipeline 0): the wave's duration in 100 MHz
- * ticks (s_memrealtime), in batch order (screen order of the batches, not dispatch order). *n_out =
- * the number of batches; up to capacity are copied. Synchronises the device. The longest batch is the
- * launch's critical path (what an N-GPU split of the frame cannot go below). */
-int rt_batch_durations(rt_scene *scene, uint32_t *ticks, int64_t capacity, int64_t *n_out);
-/* The render workspace of one pipeline for `cap` samples, `steps` = max_lvl + 1 chain steps and
- * `lights` lights, as the library carves it (no allocation, no device): total bytes and, per array
- * in carving order, (offset, bytes): q_org[0], q_dst[0], q_org[1], q_dst[1], hit_idx, hit_I, sq_org,
- * sq_dst, shadow, chain_local, chain_coef, depth, counters[0], counters[1], wq, cost[0], order[0],
- * cost[1], order[1], order_scratch. For tests of the sizing. */
-#define RT_WS_ARRAYS 20
-int rt_workspace_layout(int64_t cap, int32_t steps, int32_t lights, uint64_t *total_bytes,
-                        uint64_t extents[2 * RT_WS_ARRAYS]);
+/* Launch-shape tuning and the diagnostics of the tuning work (rt_scene_tune, rt_scene_trials,
+ * rt_batch_durations, rt_work_detail, rt_diag_read, rt_workspace_layout) are declared in
+ * raytracert_tune.h: they are not part of the drop-in contract, and no result depends on them. */
 
 #ifdef __cplusplus
 }

@@ -186,7 +186,6 @@ class RayTracer {
     rt_scene *scene() const { return scene_; }
 
     rt_params params() const {
-        if (MyLightPositions.size() > RT_MAX_LIGHTS) throw Error(RT_E_ARG, "at most 16 lights");
         rt_params p{};
         p.width = static_cast<int32_t>(WindowSize_X);
         p.height = static_cast<int32_t>(WindowSize_Y);
@@ -195,9 +194,12 @@ class RayTracer {
         p.max_lvl = max_lvl;
         p.flags = (Ambient ? RT_AMBIENT : 0u) | (Diffuse ? RT_DIFFUSE : 0u) | (Specular ? RT_SPECULAR : 0u) |
                   (Reflection ? RT_REFLECTION : 0u) | (Shadows ? RT_SHADOWS : 0u) | (Refraction ? RT_REFRACTION : 0u);
+        // any number of lights (the reference's list is an unbounded vector): the first RT_MAX_LIGHTS
+        // inline, and the whole list through light_list (Vec3Df is three packed floats), read during the call
         p.n_lights = static_cast<int32_t>(MyLightPositions.size());
-        for (size_t i = 0; i < MyLightPositions.size(); ++i)
+        for (size_t i = 0; i < MyLightPositions.size() && i < RT_MAX_LIGHTS; ++i)
             for (int k = 0; k < 3; ++k) p.lights[i][k] = MyLightPositions[i][k];
+        if (MyLightPositions.size() > RT_MAX_LIGHTS) p.light_list = MyLightPositions[0].p;
         for (int k = 0; k < 3; ++k) p.camera_pos[k] = MyCameraPosition[k];
         return p;
     }

@@ -30,12 +30,14 @@
  *
  * performRayTracing and the 'r' loop: a call whose (origin, dest) is the first sub-sample of the
  * loop main.cpp:369-388 runs for the current corner rays (produceRay) makes the header trace every
- * sub-sample of that frame in one GPU call (rt_trace_rays over the loop's own rays, computed with
- * the loop's own float expressions); the loop's later calls are answered from it while each
- * (origin, dest) and every parameter the trace reads equal the prediction bit for bit, and any other
- * call is traced on its own. The colours are those of the per-call path either way (the same
- * rt_trace_rays arithmetic; tests/test_cxx_dropin.py checks both against the oracle); the unchanged
- * loop just stops paying one GPU round trip per sub-sample (RTAMD_DROPIN_NO_FRAME_CACHE turns it off).
+ * sub-sample of that frame in one GPU call (rt_trace_frame_samples: the device makes the loop's rays
+ * with the loop's own binary32 expressions and returns, per sub-sample in the loop's order, the ray and
+ * its colour into pinned memory); the loop's later calls are answered from it while each (origin,
+ * dest) equals the next record's ray bit for bit and every parameter the trace reads is unchanged, and
+ * any other call is traced on its own. The colours are those of the per-call path either way (each
+ * is the trace of the very ray the call passed; tests/test_cxx_dropin.py checks both against the
+ * oracle); the unchanged loop just stops paying one GPU round trip per sub-sample
+ * (RTAMD_DROPIN_NO_FRAME_CACHE turns it off).
  *
  * Extra: RayTracerDevice (the GPU init() binds; RT_HOST_ONLY = loader only), uploadMesh() (re-upload
  * MyMesh after editing it), renderImage() (the 'r' loop in one call, Image::_image's floats),
@@ -390,7 +392,6 @@ inline rt_scene *need_scene() {
 }
 // Everything the reference reads from globals during a trace.
 inline rt_params params(int levels_left) {
-    if (MyLightPositions.size() > RT_MAX_LIGHTS) throw Error(RT_E_ARG, "at most 16 lights");
     rt_params p{};
     p.width = static_cast<int32_t>(WindowSize_X);
     p.height = static_cast<int32_t>(WindowSize_Y);
@@ -399,9 +400,13 @@ inline rt_params params(int levels_left) {
     p.max_lvl = levels_left;
     p.flags = (Ambient ? RT_AMBIENT : 0u) | (Diffuse ? RT_DIFFUSE : 0u) | (Specular ? RT_SPECULAR : 0u) |
               (Reflection ? RT_REFLECTION : 0u) | (Shadows ? RT_SHADOWS : 0u) | (Refraction ? RT_REFRACTION : 0u);
+    // any number of lights, as the reference's unbounded list ('L' appends one, main.cpp:334-336): the
+    // first RT_MAX_LIGHTS inline, the whole list through light_list (Vec3Df is three packed floats; read
+    // during the call that takes these params)
     p.n_lights = static_cast<int32_t>(MyLightPositions.size());
-    for (size_t i = 0; i < MyLightPositions.size(); ++i)
+    for (size_t i = 0; i < MyLightPositions.size() && i < RT_MAX_LIGHTS; ++i)
         for (int k = 0; k < 3; ++k) p.lights[i][k] = MyLightPositions[i][k];
+    if (MyLightPositions.size() > RT_MAX_LIGHTS) p.light_list = MyLightPositions[0].p;
     for (int k = 0; k < 3; ++k) p.camera_pos[k] = MyCameraPosition[k];
     p.seed = RT_DEFAULT_SEED;
     return p;
@@ -529,9 +534,17 @@ struct TraceState {
         if (scene != rtamd_dropin::scene() || gen != scene_generation() || amb != Ambient || dif != Diffuse ||
             refl != Reflection || sha != Shadows || spec != Specular || refr != Refraction || pfx != pixelfactorX ||
             pfy != pixelfactorY || w != WindowSize_X || h != WindowSize_Y || lvl != max_lvl ||
-            lights.size() != MyLightPositions.size() || std::memcmp(cam.p, MyCameraPosition.p, sizeof cam.p) != 0)
+            lights.size() != MyLightPositions.size() || !same_bits3(cam.p, MyCameraPosition.p))
             return false;
-        return lights.empty() || std::memcmp(lights.data(), MyLightPositions.data(), sizeof(Vec3Df) * lights.size()) == 0;
+        for (size_t i = 0; i < lights.size(); ++i)
+            if (!same_bits3(lights[i].p, MyLightPositions[i].p)) return false;
+        return true;
+    }
+    static bool same_bits3(const float *a, const float *b) {
+        uint32_t u[3], v[3];
+        std::memcpy(u, a, 12);
+        std::memcpy(v, b, 12);
+        return ((u[0] ^ v[0]) | (u[1] ^ v[1]) | (u[2] ^ v[2])) == 0;
     }
 };
 
@@ -546,52 +559,71 @@ inline void loop_ray(unsigned x, unsigned y, int subx, int suby, float divX, flo
     dest = yscale * (xscale * c[1] + (1 - xscale) * c[5]) + (1 - yscale) * (xscale * c[3] + (1 - xscale) * c[7]);
 }
 
-// Every sub-sample colour of one 'r' frame, in the loop's call order (y, x, subx, suby).
+// One 'r' frame's sub-samples, traced on the device in one call (rt_trace_frame_samples with
+// RT_SAMPLES_RAY_RGB): per call of the loop, in its order, the ray the device made for it with the
+// loop's own expressions and that ray's colour. Call `next` is answered from record `next` when its
+// (origin, dest) equals the record's ray bit for bit: the colour is then exactly trace() of the
+// call's own ray, whatever compiler flags the host loop was built with (a host whose floats differ
+// just misses and takes the per-call path).
 struct FrameCache {
     TraceState state;
-    std::vector<Vec3Df> org, dst, rgb;
-    size_t next = 0;
+    size_t n = 0, next = 0;   // records in the frame; the next call's record
+    float *rec = nullptr;     // 9 floats per sub-sample: origin, dest, rgb (pinned host memory)
+    size_t rec_cap = 0;
+    ~FrameCache() { rt_host_free(rec); }
+    bool matches(const Vec3Df &o, const Vec3Df &d) const {   // the call's ray is record `next`'s, bit for bit
+        uint32_t a[6], b[6];
+        std::memcpy(a, o.p, 12);
+        std::memcpy(a + 3, d.p, 12);
+        std::memcpy(b, rec + 9 * next, 24);
+        uint32_t x = 0;
+        for (int i = 0; i < 6; ++i) x |= a[i] ^ b[i];
+        return x == 0;
+    }
+    Vec3Df take() {
+        const float *c = rec + 9 * next++ + 6;
+        return Vec3Df(c[0], c[1], c[2]);
+    }
 };
 inline FrameCache &frame_cache() {
     static FrameCache c;
     return c;
 }
 
-// If (origin, dest) is the first sub-sample of the 'r' loop for the current corner rays, trace the
-// whole frame's sub-samples in one GPU call (chunks of 2^22 rays) into the cache and return true.
+// If (origin, dest) is the first sub-sample of the 'r' loop for the current corner rays (produceRay),
+// trace every sub-sample of that frame in one GPU call into the cache and return true.
 inline bool start_frame(const Vec3Df &origin, const Vec3Df &dest) {
     if (!produceRay || WindowSize_X == 0 || WindowSize_Y == 0 || pixelfactorX == 0 || pixelfactorY == 0 || !scene())
         return false;
     Vec3Df c[8];   // origin00, dest00, origin01, dest01, origin10, dest10, origin11, dest11 (main.cpp:355-358)
     produceRay(0, 0, c[0], c[1]);
-    float divX = (WindowSize_X * pixelfactorX - 1);
-    float divY = (WindowSize_Y * pixelfactorY - 1);
-    Vec3Df o0, d0;
     produceRay(0, WindowSize_Y - 1, c[2], c[3]);
     produceRay(WindowSize_X - 1, 0, c[4], c[5]);
     produceRay(WindowSize_X - 1, WindowSize_Y - 1, c[6], c[7]);
+    float divX = (WindowSize_X * pixelfactorX - 1);
+    float divY = (WindowSize_Y * pixelfactorY - 1);
+    Vec3Df o0, d0;
     loop_ray(0, 0, 0, 0, divX, divY, c, o0, d0);
-    if (!same_bits(o0, origin) || !same_bits(d0, dest)) return false;
-    const size_t n = static_cast<size_t>(WindowSize_X) * WindowSize_Y * pixelfactorX * pixelfactorY;
+    if (!same_bits(o0, origin) || !same_bits(dest, d0)) return false;
     FrameCache &fc = frame_cache();
-    fc.org.resize(n);
-    fc.dst.resize(n);
-    fc.rgb.resize(n);
-    size_t k = 0;
-    for (unsigned int y = 0; y < WindowSize_Y; ++y)
-        for (unsigned int x = 0; x < WindowSize_X; ++x)
-            for (int subx = 0; subx < static_cast<int>(pixelfactorX); subx++)
-                for (int suby = 0; suby < static_cast<int>(pixelfactorY); suby++, ++k)
-                    loop_ray(x, y, subx, suby, divX, divY, c, fc.org[k], fc.dst[k]);
-    const rt_params p = params(max_lvl);
-    constexpr size_t kChunk = size_t(1) << 22;
-    for (size_t b = 0; b < n; b += kChunk) {
-        const int32_t m = static_cast<int32_t>(std::min(kChunk, n - b));
-        check(rt_trace_rays(scene(), &p, fc.org[b].p, fc.dst[b].p, m, fc.rgb[b].p, nullptr));
+    fc.n = fc.next = 0;
+    const size_t n = static_cast<size_t>(WindowSize_X) * WindowSize_Y * pixelfactorX * pixelfactorY;
+    if (9 * n > fc.rec_cap) {
+        rt_host_free(fc.rec);
+        fc.rec = nullptr;
+        fc.rec_cap = 0;
+        void *m = nullptr;
+        check(rt_host_alloc(9 * n * sizeof(float), &m));
+        fc.rec = static_cast<float *>(m);
+        fc.rec_cap = 9 * n;
     }
+    rt_params p = params(max_lvl);
+    for (int i = 0; i < 8; ++i)
+        for (int k = 0; k < 3; ++k) p.corners[i][k] = c[i][k];
+    check(rt_trace_frame_samples(scene(), &p, RT_SAMPLES_RAY_RGB, fc.rec, fc.rec_cap, nullptr));
     fc.state = TraceState::now();
-    fc.next = 0;
-    return true;
+    fc.n = n;
+    return fc.matches(origin, dest);   // (the device's first ray is the loop's: else the per-call path)
 }
 }  // namespace rtamd_dropin
 
@@ -601,10 +633,8 @@ inline Vec3Df performRayTracing(const Vec3Df &origin, const Vec3Df &dest) {
 #ifndef RTAMD_DROPIN_NO_FRAME_CACHE
     using namespace rtamd_dropin;
     FrameCache &fc = frame_cache();
-    if (fc.next < fc.org.size() && same_bits(origin, fc.org[fc.next]) && same_bits(dest, fc.dst[fc.next]) &&
-        fc.state.matches_globals())
-        return fc.rgb[fc.next++];
-    if (start_frame(origin, dest)) return fc.rgb[fc.next++];
+    if (fc.next < fc.n && fc.matches(origin, dest) && fc.state.matches_globals()) return fc.take();
+    if (start_frame(origin, dest)) return fc.take();
 #endif
     return trace(origin, dest, 0);
 }

@@ -26,6 +26,7 @@ class OraParams(C.Structure):
         ("lights", (C.c_float * 3) * MAX_LIGHTS),
         ("camera_pos", C.c_float * 3),
         ("corners", (C.c_float * 3) * 8),
+        ("light_list", C.c_void_p),   # n_lights x 3 floats (any count) or NULL
     ]
 
 
@@ -93,9 +94,13 @@ def make_params(width, height, pf=1, max_lvl=0, lights=((0.0, 0.0, 4.0),), flags
     p.width, p.height, p.pfx, p.pfy = width, height, pf, pf if pfy is None else pfy
     p.max_lvl, p.flags, p.n_lights = max_lvl, flags, len(lights)
     p.seed = seed
-    for i, l in enumerate(lights):
+    for i, l in enumerate(lights[:MAX_LIGHTS]):
         for k in range(3):
             p.lights[i][k] = l[k]
+    if len(lights) > MAX_LIGHTS:   # the reference's light list is unbounded: the rest through light_list
+        arr = np.ascontiguousarray(np.asarray(lights, np.float32).reshape(len(lights), 3))
+        p._light_list_keepalive = arr
+        p.light_list = arr.ctypes.data
     for k in range(3):
         p.camera_pos[k] = camera_pos[k]
     cs = default_corners(width, height) if corners is None else np.asarray(corners, np.float32)

@@ -436,7 +436,9 @@ static int is_shadow(ctx *c, vec3 intersection, vec3 light_pos) {
         }
         if (c->dbg && c->dbg_n >= 1 && c->dbg_n <= c->dbg_max) {
             ora_debug_bounce *b = &c->dbg[c->dbg_n - 1];   /* the trace whose shade() asks */
-            if (blocked) b->shadowed |= 1u << c->cur_light; else b->lit |= 1u << c->cur_light;
+            if (c->cur_light < 32) {   /* (the record's masks hold lights 0-31) */
+                if (blocked) b->shadowed |= 1u << c->cur_light; else b->lit |= 1u << c->cur_light;
+            }
         }
         return blocked;
     }
@@ -501,7 +503,9 @@ static vec3 shade(ctx *c, vec3 ray, vec3 vertexPos, vec3 *normal, const material
     vec3 pixelcolor = V(0, 0, 0);
     if (feat(c, ORA_AMBIENT) && (m->flags & ORA_HAS_KA)) pixelcolor = vadd(pixelcolor, m->Ka);
     for (int i = 0; i < c->pr->n_lights; i++) {
-        vec3 L = V(c->pr->lights[i][0], c->pr->lights[i][1], c->pr->lights[i][2]);
+        /* MyLightPositions[i] (raytracing.h:9, an unbounded vector): the inline array or light_list */
+        const float *li = c->pr->light_list ? c->pr->light_list + 3 * (size_t)i : c->pr->lights[i];
+        vec3 L = V(li[0], li[1], li[2]);
         c->cur_light = i;
         if (!is_shadow(c, vertexPos, L)) {
             if (feat(c, ORA_DIFFUSE) && (m->flags & ORA_HAS_KD))

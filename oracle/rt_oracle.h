@@ -49,6 +49,7 @@ typedef struct {
     float lights[ORA_MAX_LIGHTS][3];
     float camera_pos[3];          /* MyCameraPosition */
     float corners[8][3];          /* origin00,dest00, origin01,dest01, origin10,dest10, origin11,dest11 (main.cpp:348-358) */
+    const float *light_list;      /* non-NULL: n_lights x 3 floats, any count (lights[][] ignored) */
 } ora_params;
 
 /* Material as loaded (mesh.h:10-125): 3+3+3 floats, Ns, Ni, Tr, illum, flags. */

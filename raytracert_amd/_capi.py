@@ -13,6 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # RTAMD_LIB selects another in-tree build of the same library (A/B of kernel variants, tools/)
 LIB_PATH = os.environ.get("RTAMD_LIB") or os.path.join(HERE, "librtamd.so")
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "raytracert.h")
+TUNE_HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "raytracert_tune.h")   # tuning + diagnostics
 
 RT_OK = 0
 RT_E_IO = -1
@@ -24,7 +25,10 @@ RT_E_NODEV = -6
 RT_E_RCCL = -7
 COMM_ID_BYTES = 128
 RT_HOST_ONLY = -1
-RT_MAX_LIGHTS = 16
+RT_MAX_LIGHTS = 16        # lights held inline in rt_params; more through rt_params.light_list
+RT_LIGHTS_LIMIT = 65536
+RT_TRIAL_INFO_FIELDS, RT_MAX_TRIALS = 6, 10
+SAMPLES_RGB, SAMPLES_RAY_RGB = 3, 9   # rt_trace_frame_samples record layouts
 RT_WS_ARRAYS = 20   # rt_workspace_layout arrays
 
 AMBIENT, DIFFUSE, SPECULAR, REFLECTION, SHADOWS, REFRACTION = (1 << i for i in range(6))
@@ -44,6 +48,7 @@ TUNE_STEAL_HALF, TUNE_STEAL_QUARTER = 22, 23
 TUNE_SPLIT_EIGHTH, TUNE_PRIORITY_BATCHES, TUNE_PIXEL_ORDER, TUNE_DYN_GROUP = 26, 27, 28, 29
 TUNE_SHADOW_HELPERS = 30
 TUNE_FRAMES_IN_FLIGHT = 31
+TUNE_ADOPT_ORDER = 32
 BVH_INFO_FIELDS = 7
 STOCHASTIC = 1 << 8
 DEFAULT_SEED = 0x5EED
@@ -60,6 +65,7 @@ class RtParams(C.Structure):
         ("lights", (C.c_float * 3) * RT_MAX_LIGHTS),
         ("camera_pos", C.c_float * 3),
         ("corners", (C.c_float * 3) * 8),
+        ("light_list", C.c_void_p),   # n_lights x 3 floats (any count) or NULL: lights[0..n_lights)
     ]
 
 
@@ -100,6 +106,9 @@ _SIGNATURES = {
     "rt_trace_rays": ([_VP, C.POINTER(RtParams), _VP, _VP, C.c_int32, _VP, _VP], C.c_int),
     "rt_debug_trace": ([_VP, C.POINTER(RtParams), _VP, _VP, _VP, C.c_int32, C.POINTER(C.c_int32), _VP], C.c_int),
     "rt_render_tile": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP, _VP, _VP], C.c_int),
+    "rt_trace_frame_samples": ([_VP, C.POINTER(RtParams), C.c_int32, _VP, C.c_size_t, _VP], C.c_int),
+    "rt_host_alloc": ([C.c_size_t, C.POINTER(_VP)], C.c_int),
+    "rt_host_free": ([_VP], None),
     "rt_render_frame_device": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, _VP, C.c_size_t, _VP, _VP], C.c_int),
     "rt_render_tiles_device": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP,
                                 C.c_size_t, _VP, C.POINTER(C.c_int32), _VP], C.c_int),
@@ -135,9 +144,11 @@ _SIGNATURES = {
 _lib = None
 
 
-def header_symbols(path: str = HEADER_PATH) -> list[str]:
-    """Function names declared in include/raytracert.h."""
-    text = open(path).read()
+def header_symbols(paths=(HEADER_PATH, TUNE_HEADER_PATH)) -> list[str]:
+    """Function names declared in include/raytracert.h and include/raytracert_tune.h."""
+    if isinstance(paths, str):
+        paths = (paths,)
+    text = "".join(open(p).read() for p in paths)
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(rt_[a-z_0-9]+)\s*\(", text)))
 

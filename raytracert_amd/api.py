@@ -54,15 +54,22 @@ class RenderParams:
     pfy: int | None = None           # pixelfactorY when it differs from pixelfactorX (= pf)
 
     def to_c(self) -> RtParams:
-        if len(self.lights) > _capi.RT_MAX_LIGHTS:
-            raise ValueError("at most 16 lights")
+        """The C struct. Up to RT_MAX_LIGHTS lights go inline; more go through light_list, a float32
+        array kept alive on the returned struct (the reference's light list is unbounded)."""
+        n = len(self.lights)
+        if n > _capi.RT_LIGHTS_LIMIT:
+            raise ValueError(f"at most {_capi.RT_LIGHTS_LIMIT} lights")
         p = RtParams()
         p.width, p.height, p.pfx, p.pfy = self.width, self.height, self.pf, self.pf if self.pfy is None else self.pfy
-        p.max_lvl, p.flags, p.n_lights = self.max_lvl, self.flags, len(self.lights)
+        p.max_lvl, p.flags, p.n_lights = self.max_lvl, self.flags, n
         p.seed = int(self.seed)
-        for i, l in enumerate(self.lights):
+        for i, l in enumerate(self.lights[:_capi.RT_MAX_LIGHTS]):
             for k in range(3):
                 p.lights[i][k] = float(l[k])
+        if n > _capi.RT_MAX_LIGHTS:
+            arr = np.ascontiguousarray(np.asarray(self.lights, np.float32).reshape(n, 3))
+            p._light_list_keepalive = arr
+            p.light_list = arr.ctypes.data
         for k in range(3):
             p.camera_pos[k] = float(self.camera_pos[k])
         cs = default_corners(self.width, self.height) if self.corners is None else np.asarray(self.corners, np.float32)
@@ -206,6 +213,18 @@ class Scene:
         check(lib().rt_render_tile(self._h, C.byref(p), x0, y0, w, h, _ptr(u8), _ptr(f32), _ptr(counts)))
         return u8, f32, counts
 
+    def trace_frame_samples(self, params: RenderParams, with_rays: bool = False):
+        """rt_trace_frame_samples: performRayTracing of every sub-sample of the 'r' loop (main.cpp:369-388),
+        unclamped, in the loop's call order: rec[height, width, pfx, pfy, 3] float32 (the colour), or with
+        with_rays [..., 9] (origin, dest, colour); and counts[3]."""
+        pfy = params.pf if params.pfy is None else params.pfy
+        layout = _capi.SAMPLES_RAY_RGB if with_rays else _capi.SAMPLES_RGB
+        rec = np.zeros((params.height, params.width, params.pf, pfy, layout), np.float32)
+        counts = np.zeros(3, np.uint64)
+        p = params.to_c()
+        check(lib().rt_trace_frame_samples(self._h, C.byref(p), layout, _ptr(rec), rec.size, _ptr(counts)))
+        return rec, counts
+
     def render_tiles_device(self, params: RenderParams | RtParams, tile_w: int, tile_h: int, first: int, stride: int,
                             out_ptr: int, out_capacity: int, stream_ptr: int | None = None, want_counts: bool = False,
                             frames: int = 1):
@@ -279,18 +298,20 @@ class Scene:
              "forget_order": _capi.TUNE_FORGET_ORDER, "split_eighth": _capi.TUNE_SPLIT_EIGHTH,
              "prio_batches": _capi.TUNE_PRIORITY_BATCHES,
              "pixel_order": _capi.TUNE_PIXEL_ORDER, "dyn_group": _capi.TUNE_DYN_GROUP,
-             "shadow_helpers": _capi.TUNE_SHADOW_HELPERS, "frames_in_flight": _capi.TUNE_FRAMES_IN_FLIGHT}[knob]
+             "shadow_helpers": _capi.TUNE_SHADOW_HELPERS, "frames_in_flight": _capi.TUNE_FRAMES_IN_FLIGHT,
+             "adopt_order": _capi.TUNE_ADOPT_ORDER}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
 
     def trials(self) -> dict:
         """rt_scene_trials: the per-view launch trials (steal x distribution x shadow helpers) of
         pipeline 0."""
-        info = np.zeros(5, np.int32)
-        ms = np.zeros(8, np.float32)
+        info = np.zeros(_capi.RT_TRIAL_INFO_FIELDS, np.int32)
+        ms = np.zeros(_capi.RT_MAX_TRIALS, np.float32)
         check(lib().rt_scene_trials(self._h, info.ctypes.data, ms.ctypes.data))
         n = int(info[0])
         return {"trials": n, "choice": int(info[1]), "wave_steal": int(info[2]), "chain_split": int(info[3]),
-                "shadow_helpers": int(info[4]), "trial_ms": [round(float(x), 4) for x in ms[:n]]}
+                "shadow_helpers": int(info[4]), "steal_quarter": int(info[5]),
+                "trial_ms": [round(float(x), 4) for x in ms[:n]]}
 
     def batch_durations(self) -> np.ndarray:
         """Per wave batch of the latest chain launch: the wave's duration in microseconds

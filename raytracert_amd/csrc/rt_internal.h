@@ -6,7 +6,7 @@
 #include <string>
 #include <vector>
 
-#include "raytracert.h"
+#include "raytracert_tune.h"   // (includes raytracert.h)
 
 namespace rt {
 

@@ -22,10 +22,12 @@ struct FrameGeom {
     int32_t first, stride;              // tile id of batch tile i = first + (tile0 + i) * stride
     int32_t tile0, ntiles;              // this batch
     int32_t ox, oy, cw, ch;             // tiled region origin / clip size (absolute pixels)
-    int32_t out_mode;                   // 0: tile-major shard layout, 1: row-major in the clip rect
+    int32_t out_mode;                   // 0: tile-major shard layout, 1: row-major in the clip rect, 2: every
+                                        // sub-sample's unclamped colour, row-major pixels x (subx, suby) (f32)
     int32_t tiles_total;                // tiles per frame: ids wrap modulo this (multi-frame batches)
     int32_t stochastic;                 // RT_STOCHASTIC: jittered sub-samples
     uint32_t seed;                      // its hash seed
+    int32_t sample_stride;              // out_mode 2: floats per sample record (3: rgb; 9: origin, dest, rgb)
     int32_t pix_order;                  // pixels of a tile in sample order: 0 row-major, 1 Morton (square
                                         // power-of-two tiles: a 64-sample batch covers 8x8 pixels)
     float corners[8][3];                // origin00,dest00,origin01,dest01,origin10,dest10,origin11,dest11
@@ -38,9 +40,10 @@ struct ShadeParams {
     uint32_t flags;
     int32_t n_lights;
     int32_t step;
-    float lights[RT_MAX_LIGHTS][3];
+    float lights[RT_MAX_LIGHTS][3];     // the first RT_MAX_LIGHTS lights
     float cam[3];
     float pad;
+    const float *light_ext;             // n_lights > RT_MAX_LIGHTS: all n_lights x 3 (device), else null
 };
 
 // Where a shadow kernel's queries come from (isShadow, raytracing.cpp:241-261). Compacted: the
@@ -56,6 +59,7 @@ struct ShadowSource {
     int32_t *pair_count;
     int32_t n_lights, virt;
     float lights[RT_MAX_LIGHTS][3];
+    const float *light_ext;         // as ShadeParams::light_ext
 };
 
 // Device views of one scene and one render workspace.
@@ -128,7 +132,9 @@ constexpr int kWaveQueueSlot = kMaxStepsCounters - kWqSlot;
 // k_gen_primary zeroes w.counters (then counter 0 = the batch's samples) and w.wq, and writes the
 // step-0 queue of primary rays; resets_only (a fused chain launch follows, which makes its primary
 // rays itself): only the resets.
-void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream, bool resets_only = false);
+// samples (out_mode 2, sample_stride 9): each valid sample's ray goes to its record too.
+void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream, bool resets_only = false,
+                        float *samples = nullptr);
 void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevWork &w, hipStream_t stream);
 void launch_closest_hit(const DevScene &s, const DevWork &w, int step, int64_t capacity, hipStream_t stream);
 void launch_shadow_gen(const DevScene &s, const DevWork &w, const ShadeParams &p, int64_t capacity, hipStream_t stream);
@@ -157,6 +163,7 @@ void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t strea
 constexpr int kOrderBuckets = 128;
 constexpr uint32_t kCostSplit = 0x80000000u;   // batch_cost flag: the batch ran split (lifetime in bits 0-30)
 constexpr int kWaveBatch = 64;   // lanes per wave batch of the chain launch (one sample per lane)
+constexpr int kChainMaxLights = 32;   // the chain launch's per-step shadow mask; more lights: per-step kernels
 hipError_t launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream);
 // A cold launch's batch scores (no measured order yet): one primary walk per wave batch of a fused
 // launch (g, fuse_spp, capacity as launch_chain's), scored into score[batch] for launch_order_batches.

@@ -48,6 +48,16 @@ __device__ __forceinline__ void normalize(V3 &a) {                              
 __device__ __forceinline__ float max_std(float a, float b) { return (a < b) ? b : a; }            // std::max
 __device__ __forceinline__ V3 ld3(const float4 &v) { return mk(v.x, v.y, v.z); }
 
+// Light l (MyLightPositions[l], raytracing.h:9): the first RT_MAX_LIGHTS ride in the kernel arguments,
+// the rest (an unbounded list, as the reference's std::vector) come from the device copy light_ext.
+__device__ __forceinline__ V3 light_at(const float (&inl)[RT_MAX_LIGHTS][3], const float *ext, int l) {
+    if (l < RT_MAX_LIGHTS) return mk(inl[l][0], inl[l][1], inl[l][2]);
+    return mk(ext[3 * l], ext[3 * l + 1], ext[3 * l + 2]);
+}
+// (The chain launch carries one chain step's shadow verdicts as a 32-bit mask, so it serves up to 32
+// lights, kChainMaxLights; with more, up to RT_LIGHTS_LIMIT, the render runs the per-step kernels,
+// whose verdicts are bytes per (query, light) in the workspace: rt_capi.cpp run_chain.)
+
 // acosf(check) in (0, 2] for check < 0 (raytracing.cpp:296-298): glibc's acosf crosses 2.0
 // exactly once on [-1, 0), at -0x1.aa226cp-2 (acosf of it is 2.0f); verified exhaustively by
 // tests/test_numerics.py::test_acos_threshold against this platform's libm.
@@ -925,7 +935,8 @@ __device__ __forceinline__ bool shadow_query(const ShadowSource &src, int j, int
         if (src.hit_idx[k] < 0) return false;
         const float4 I = src.hit_I[k];
         o = mk(I.x + 0.1f, I.y + 0.1f, I.z + 0.1f);                                    // :248
-        dir = mk(src.lights[l][0] - o.x, src.lights[l][1] - o.y, src.lights[l][2] - o.z);
+        const V3 Lp = light_at(src.lights, src.light_ext, l);
+        dir = mk(Lp.x - o.x, Lp.y - o.y, Lp.z - o.z);
         slot = j;
         return true;
     }
@@ -1164,7 +1175,7 @@ __device__ __forceinline__ bool primary_sample(const FrameGeom &g, int64_t s, V3
 // Also resets the batch's queue counters and work-queue slots (counter 0 = the queue's size), so
 // no separate fills precede the batch. resets_only (the fused chain launch follows, which makes
 // each primary ray in its lane with primary_sample and writes the pixels itself): nothing else.
-__global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWork w, int resets_only) {
+__global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWork w, int resets_only, float *__restrict__ samples) {
     const int spp = g.pfx * g.pfy;
     const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th * spp;
     const int64_t s = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
@@ -1175,6 +1186,10 @@ __global__ __launch_bounds__(kBlock) void k_gen_primary(const FrameGeom g, DevWo
     int64_t px;
     int sub;
     const bool valid = primary_sample(g, s, origin, dest, px, sub);
+    if (samples && valid) {   // out_mode 2 records with rays (rt_trace_frame_samples, RT_SAMPLES_RAY_RGB)
+        float *r = samples + static_cast<int64_t>(g.sample_stride) * (px * g.pfx * g.pfy + sub);
+        r[0] = origin.x; r[1] = origin.y; r[2] = origin.z; r[3] = dest.x; r[4] = dest.y; r[5] = dest.z;
+    }
     w.depth[s] = 0;
     w.q_org[0][s] = make_float4(origin.x, origin.y, origin.z, as_float(static_cast<int>(s)));
     w.q_dst[0][s] = make_float4(dest.x, dest.y, dest.z, as_float(valid ? 0 : -1));
@@ -1214,7 +1229,8 @@ __global__ __launch_bounds__(kBlock) void k_shadow_gen(const ShadeParams p, DevW
             const int j = slot / L, l = slot - j * L;
             const float4 I = w.hit_I[j];
             w.sq_org[pos[k]] = make_float4(I.x + 0.1f, I.y + 0.1f, I.z + 0.1f, as_float(slot));
-            w.sq_dst[pos[k]] = make_float4(p.lights[l][0], p.lights[l][1], p.lights[l][2], 0.0f);
+            const V3 Lp = light_at(p.lights, p.light_ext, l);
+            w.sq_dst[pos[k]] = make_float4(Lp.x, Lp.y, Lp.z, 0.0f);
         }
     }
 }
@@ -1306,7 +1322,7 @@ __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadePa
     V3 color = mk(0, 0, 0);                                          // :336
     if ((f & RT_AMBIENT) && (m.flags & RT_HAS_KA)) color = add(color, Ka);   // :337-340
     for (int l = 0; l < p.n_lights; ++l) {                           // :342
-        const V3 L = mk(p.lights[l][0], p.lights[l][1], p.lights[l][2]);
+        const V3 L = light_at(p.lights, p.light_ext, l);
         const bool shadowed = (f & RT_SHADOWS) ? is_shadowed(l) : false;
         if (shadowed) continue;
         if ((f & RT_DIFFUSE) && (m.flags & RT_HAS_KD)) {             // diffuseOnly :197-205
@@ -1530,7 +1546,8 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
         for (int l = role; l < p.n_lights; l += roles) {
             int sidx = -1;
             V3 sI = mk(0, 0, 0);
-            const V3 sd = mk(p.lights[l][0] - so.x, p.lights[l][1] - so.y, p.lights[l][2] - so.z);
+            const V3 Lp = light_at(p.lights, p.light_ext, l);
+            const V3 sd = mk(Lp.x - so.x, Lp.y - so.y, Lp.z - so.z);
             bvh_query_w<kAnyHit, W, kSteal>(sc, so, sd, true, sidx, sI, stack, ws.tests, ws.visits);
             if (sidx >= 0 && !sc.mats[sc.tri_mat[sidx]].transparent) mask |= 1u << l;   // :253-257
         }
@@ -1619,7 +1636,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         const int j = pb * spb + lane_off;   // this lane's sample (kInLane) or queue entry
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         V3 rgb = mk(0, 0, 0);   // fused pixels: this lane's folded chain and its pixel (valid samples)
-        int px = -1;
+        int px = -1;   // (out_mode 2: the sample's output slot, pixel x spp + sub-sample)
         // shadow helpers (RT_TUNE_SHADOW_HELPERS): in a split wave of the fused launch the lanes past
         // the part's plen samples help their owners' shadow walks, roles = lanes per sample (<= lights)
         const int roles = (kInLane && !kSteal && nparts > 1 && sc.shadow_helpers && (p.flags & RT_SHADOWS))
@@ -1641,7 +1658,11 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
                 if (role) own = o;
             }
             if (!own || (role == 0 && !lane_on)) return;
-            if (role == 0) px = static_cast<int>(pxi);
+            if (role == 0) px = g.out_mode == 2 ? static_cast<int>(pxi) * fuse_spp + sub : static_cast<int>(pxi);
+            if (g.out_mode == 2 && g.sample_stride == 9 && role == 0) {   // the record's ray (RT_SAMPLES_RAY_RGB)
+                float *r = out_f32 + 9 * static_cast<int64_t>(px);
+                r[0] = org.x; r[1] = org.y; r[2] = org.z; r[3] = dst.x; r[4] = dst.y; r[5] = dst.z;
+            }
             lvl = 0;
             sample = j;
         } else {
@@ -1674,7 +1695,12 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
             lvl = sec.lvl;
         }
         }();
-        if (kInLane) {   // k_frame's arithmetic: a pixel's fuse_spp sub-samples sit in adjacent lanes
+        if (kInLane && g.out_mode == 2) {   // every sub-sample's own colour (rt_trace_frame_samples)
+            if (px >= 0) {
+                float *o = out_f32 + static_cast<int64_t>(g.sample_stride) * px + (g.sample_stride - 3);
+                o[0] = rgb.x; o[1] = rgb.y; o[2] = rgb.z;
+            }
+        } else if (kInLane) {   // k_frame's arithmetic: a pixel's fuse_spp sub-samples sit in adjacent lanes
             V3 acc = mk(0, 0, 0);
             for (int sub = 0; sub < fuse_spp; ++sub)   // summed in sub-sample order (main.cpp:377-391)
                 acc = add(acc, mk(__shfl(rgb.x, pix_lane + sub), __shfl(rgb.y, pix_lane + sub), __shfl(rgb.z, pix_lane + sub)));
@@ -1686,7 +1712,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         // bit 31 set for a split batch (kCostSplit): the sort counts it double, so a batch that ran
         // faster because it was split (or helped) stays at the head of the order instead of
         // dropping out of the split tier and back in on every re-sort
-        if (lane == 0 && wave_on) {
+        if (lane == 0 && wave_on && w.batch_cost) {   // (null: a launch with no pipeline order, rt_trace_rays)
             const uint32_t d = static_cast<uint32_t>(min(__builtin_amdgcn_s_memrealtime() - t0, 0x7FFFFFFFull));
             w.batch_cost[pb] = nparts > 1 ? (d | kCostSplit) : d;
         }
@@ -1776,6 +1802,14 @@ __global__ __launch_bounds__(kBlock) void k_frame(const FrameGeom g, DevWork w, 
         if (g.out_mode == 0 && out_u8) { out_u8[o] = 0; out_u8[o + 1] = 0; out_u8[o + 2] = 0; }
         return;
     }
+    if (g.out_mode == 2) {   // every sub-sample's own colour, unclamped (rt_trace_frame_samples)
+        for (int sub = 0; sub < spp; ++sub) {
+            const V3 c = fold_chain(w, pix * spp + sub);
+            float *q = out_f32 + static_cast<int64_t>(g.sample_stride) * (o / 3 * spp + sub) + (g.sample_stride - 3);
+            q[0] = c.x; q[1] = c.y; q[2] = c.z;
+        }
+        return;
+    }
     V3 rgb = mk(0, 0, 0);
     for (int sub = 0; sub < spp; ++sub) rgb = add(rgb, fold_chain(w, pix * spp + sub));
     const float div = static_cast<float>(spp);
@@ -1842,7 +1876,7 @@ __global__ __launch_bounds__(kOrderBlock) void k_order_scatter(const uint32_t *_
         for (int k = threadIdx.x; k < kOrderBuckets; k += kOrderBlock)
             if (h[k]) base[k] = atomicAdd(&offs[k], h[k]);
         __syncthreads();
-        if (i < n) order[base[b] + r] = i;
+        if (i < n && base[b] + r < n) order[base[b] + r] = i;   // (counts are from the histogram pass: in range)
         __syncthreads();
     }
 }
@@ -1951,12 +1985,13 @@ static FrameGeom with_divisors(FrameGeom g) {
     return g;
 }
 
-void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream, bool resets_only) {
+void launch_gen_primary(const FrameGeom &g, const DevWork &w, hipStream_t stream, bool resets_only, float *samples) {
     const int64_t n = static_cast<int64_t>(g.ntiles) * g.tw * g.th * g.pfx * g.pfy;
     if (n <= 0) return;
     const int64_t clear = std::max<int64_t>(2 * kMaxStepsCounters, 2 * static_cast<int64_t>(w.steps) * kWqSlot);
     hipLaunchKernelGGL(k_gen_primary, dim3(grid_for(resets_only ? clear : std::max(n, clear))), dim3(kBlock), 0, stream,
-                       with_divisors(g), w, resets_only ? 1 : 0);
+                       with_divisors(g), w, resets_only ? 1 : 0,
+                       (!resets_only && g.out_mode == 2 && g.sample_stride == 9) ? samples : nullptr);
 }
 
 void launch_gen_rays(const float4 *org, const float4 *dst, int32_t n, const DevWork &w, hipStream_t stream) {
@@ -2030,6 +2065,7 @@ void launch_shadow_hit(const DevScene &s, const DevWork &w, const ShadeParams &p
     src.virt = virt ? 1 : 0;
     for (int l = 0; l < RT_MAX_LIGHTS; ++l)
         for (int k = 0; k < 3; ++k) src.lights[l][k] = p.lights[l][k];
+    src.light_ext = p.light_ext;
     if (s.use_bvh) {
         if (s.bvh_width == 4) launch_sh<4>(s, w, src, step, capacity, stream);
         else launch_sh<2>(s, w, src, step, capacity, stream);

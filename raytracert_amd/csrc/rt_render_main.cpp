@@ -47,9 +47,10 @@ int main(int argc, char **argv) {
     rt_params p{};
     p.width = w; p.height = h; p.pfx = pf; p.pfy = pf; p.max_lvl = depth; p.flags = flags;
     p.n_lights = static_cast<int>(lights.size());
-    if (p.n_lights > RT_MAX_LIGHTS) { std::fprintf(stderr, "too many lights\n"); return 2; }
+    std::vector<float> list;   // any number of lights (more than RT_MAX_LIGHTS go through light_list)
     for (int l = 0; l < p.n_lights; ++l)
-        for (int k = 0; k < 3; ++k) p.lights[l][k] = lights[l][k];
+        for (int k = 0; k < 3; ++k) list.push_back(lights[l][k]);
+    p.light_list = list.data();
     p.camera_pos[0] = 0; p.camera_pos[1] = 0; p.camera_pos[2] = 4;
     if (rt_default_corners(w, h, p.corners) != RT_OK) { std::fprintf(stderr, "%s\n", rt_last_error_string()); return 1; }
     rt_scene *scene = nullptr;

@@ -22,7 +22,9 @@ def test_library_exports_every_header_symbol():
 
 
 def test_struct_layouts_match_header():
-    assert C.sizeof(_capi.RtParams) == 4 * 8 + 16 * 12 + 12 + 8 * 12
+    # 8 int fields, 16 inline lights, camera, 8 corners, then the light_list pointer (8-aligned)
+    assert C.sizeof(_capi.RtParams) == 4 * 8 + 16 * 12 + 12 + 8 * 12 + 4 + 8
+    assert _capi.RtParams.light_list.offset == 336
     assert C.sizeof(_capi.RtMaterial) == 4 * 14
     assert C.sizeof(_capi.RtParams) == C.sizeof(O.OraParams)
 
@@ -103,7 +105,7 @@ def test_tune_knobs_validate_ranges(tmp_path):
                             ("batch_order", (0, 1), (2, 3)), ("chain_split", (0, 3, 4, 5), (6, 7, -1)),
                             ("pixel_order", (0, 1, 2), (3, -1)), ("dyn_group", (0, 2, 6), (7, -1)),
                             ("cold_estimate", (0, 1, 2), (3, -1)),
-                            ("steal_half", (0, 512, 65535), (-1, 65536)), ("steal_quarter", (0, 8, 4096), (-1, 4097)),
+                            ("steal_half", (0, 512, 65535), (-1, 65536)), ("steal_quarter", (-1, 0, 8, 4096), (-2, 4097)),
                             ("split_eighth", (0, 64, 4096), (-1, 4097)), ("prio_batches", (0, 64, 1 << 30), (-1,)),
                             ("shadow_helpers", (0, 1, 2), (3, -1)), ("frames_in_flight", (1, 2, 4), (0, 5)), ("pipes", (1, 4), (0, 5))]:
         for v in good:

@@ -153,3 +153,24 @@ def test_dropin_literal_loop_uses_one_gpu_call_per_frame(dropin_bin, workdir, tm
     assert np.array_equal(read_ppm(fr[0][1]), read_ppm(fr[1][1]))
     single = next(l.split() for l in lines if l.startswith("single "))
     assert float(single[4]) > 0
+
+
+@pytest.mark.gpu
+def test_dropin_session_with_more_lights_than_inline(dropin_bin, workdir, tmp_path, gpu_available):
+    """'L' appends a light on every press (main.cpp:334-336) and shade() loops over all of them
+    (raytracing.cpp:342): 19 presses give 20 lights (more than RT_MAX_LIGHTS, through
+    rt_params.light_list), 'r' and renderImage() render them, and 16 more presses (36 lights, the
+    per-step kernels) render again. Every frame equals the oracle's."""
+    path = scene_path("syn:F4", workdir)
+    prefix = str(tmp_path / "m")
+    keys = ["-", "-"] + ["L"] * 19 + ["r", "R"] + ["L"] * 16 + ["r"]
+    lines = _lines([dropin_bin, "keys", path, "40", "24", prefix] + keys)
+    frames = [l.split() for l in lines if l.startswith("frame ")]
+    assert len(frames) == 3
+    orc = O.OracleScene(path)
+    for f, nl in zip(frames, (20, 20, 36)):
+        if f[5] != "renderImage":
+            assert int(f[8]) == nl
+        ou8 = orc.render(O.make_params(40, 24, pf=1, max_lvl=10, lights=[(0.0, 0.0, 4.0)] * nl), nthreads=16)[1]
+        d = np.abs(read_ppm(f[1]).astype(np.int16) - ou8.astype(np.int16))
+        assert d.max() <= 1 and (d == 0).mean() >= 0.9999, f

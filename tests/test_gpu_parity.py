@@ -540,31 +540,36 @@ def test_shadow_helpers_match_plain_walk(spec, w, h, pf, lights, half, quarter, 
             assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
 
 
+@pytest.mark.parametrize("quarter,ncand", [(0, 6), (-1, 9)])
 @pytest.mark.parametrize("w,h,pf", [(400, 300, 1), (64, 48, 8), (100, 75, 3)])
-def test_wave_steal_auto_trials_keep_results(w, h, pf, workdir, gpu_available):
+def test_wave_steal_auto_trials_keep_results(w, h, pf, quarter, ncand, workdir, gpu_available):
     """RT_TUNE_WAVE_STEAL 2 with RT_TUNE_CHAIN_SPLIT 5 (the defaults) and RT_TUNE_SHADOW_HELPERS 2:
     the first launch over a frame geometry takes its batches dynamically (4), the next re-sort the
-    order each time until it was measured under a measured order, then 13 launches are the
-    timed trials (a warm-up, then two rounds over the six candidates: per distribution, plain without
-    and with shadow helpers, stealing), later ones use
-    the fastest; every render of the sequence equals the plain walk's with block dispatch (pf 8: 64
-    sub-samples per pixel, where the half-wave split must stay off), and the trials are reported."""
+    order each time until it was measured under a measured order, then 1 + 2 x candidates launches
+    are the timed trials (a warm-up, then two rounds over the candidates: per distribution, plain
+    without and with shadow helpers, stealing; with RT_TUNE_STEAL_QUARTER -1, the default, the
+    block-dispatch ones also with the quarter tier: nine), later ones use the fastest; every render of
+    the sequence equals the plain walk's with block dispatch (pf 8: 64 sub-samples per pixel, where
+    the split tiers must stay off), and the trials are reported."""
     p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=1, lights=[[0, 0, 4], [1.5, 1.5, 4]])
     with R.Scene.load(scene_path("ref:dodgeColorTest.obj", workdir), device=0) as sc:
         sc.tune("wave_steal", 0)
         sc.tune("chain_split", 0)
+        sc.tune("steal_quarter", 0)
         ref, reff, refc = sc.render(p, want_f32=True)
         sc.tune("wave_steal", 2)
         sc.tune("chain_split", 5)
         sc.tune("shadow_helpers", 2)
+        sc.tune("steal_quarter", quarter)
         sc.tune("forget_order", 1)
-        for _ in range(22):
+        for _ in range(6 + 2 * ncand):
             u8, f32, c = sc.render(p, want_f32=True)
             assert [int(x) for x in c] == [int(x) for x in refc]
             assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
         t = sc.trials()
-        assert t["trials"] == 6 and 0 <= t["choice"] < 6 and len(t["trial_ms"]) == 6
+        assert t["trials"] == ncand and 0 <= t["choice"] < ncand and len(t["trial_ms"]) == ncand
         assert t["wave_steal"] in (0, 1) and t["chain_split"] in (0, 4) and t["shadow_helpers"] in (0, 1)
+        assert t["steal_quarter"] in ((0,) if quarter == 0 else (0, 64))
 
 
 @pytest.mark.parametrize("spec,w,h,pf,pfy,flags", [("syn:C4", 333, 187, 3, 3, 0), ("syn:F4", 96, 54, 3, 3, 0),
