@@ -644,7 +644,12 @@ def strong_model(t1_ms, crit_ms, shard_ms, frame_bytes, link_gbs=(50.0, 150.0), 
     frame's longest wave batch (its critical path, measured); then one RCCL gather to rank 0 over
     xGMI (rank 0 receives frame_bytes / N from each of the N - 1 peers on its own link, at an
     assumed 50-150 GB/s per link, plus a collective latency), the device un-permute (measured at
-    N = 1: the shard path minus the frame path) and a barrier."""
+    N = 1: the shard path minus the frame path) and a barrier.
+    Two readings: `latency` is one frame on its own (render, then gather, un-permute and barrier in
+    sequence); `pipelined` is the frame rate of a stream of frames as bench.py's --mode strong runs
+    it (step i's gather runs on the collective's stream and its un-permute on rank 0's side stream
+    while step i + 1 renders, Runner.step), so the per-frame time is the slowest of the three
+    stages plus the per-step barrier."""
     assemble_ms = max(0.0, (shard_ms or t1_ms) - t1_ms)
     out = {"inputs": {"t1_ms": round(t1_ms, 4), "critical_path_ms": round(crit_ms, 4), "assemble_ms": round(assemble_ms, 4),
                       "frame_bytes": frame_bytes, "link_gbs": list(link_gbs), "rccl_latency_ms": rccl_lat_ms,
@@ -655,7 +660,9 @@ def strong_model(t1_ms, crit_ms, shard_ms, frame_bytes, link_gbs=(50.0, 150.0), 
         for bw in link_gbs:
             gather = frame_bytes / n / (bw * 1e9) * 1e3 + rccl_lat_ms
             t = render + gather + assemble_ms + sync_ms
-            res[f"{int(bw)}GBs"] = {"ms_per_frame": round(t, 4), "speedup": round(t1_ms / t, 2)}
+            tp = max(render, gather, assemble_ms) + sync_ms
+            res[f"{int(bw)}GBs"] = {"latency_ms_per_frame": round(t, 4), "latency_speedup": round(t1_ms / t, 2),
+                                    "pipelined_ms_per_frame": round(tp, 4), "pipelined_speedup": round(t1_ms / tp, 2)}
         out[f"n{n}"] = {"render_ms": round(render, 4), "bound": "critical path" if crit_ms >= t1_ms / n else "work / N", **res}
     return out
 

@@ -99,6 +99,12 @@ extern "C" {
 #define RT_TUNE_ADOPT_ORDER 32   /* 1 (default): a pipeline meeting a batch geometry that another pipeline has
                                     already ordered starts from that pipeline's measured order (frames in
                                     flight); 0: it learns its own from a cold launch. Placement only */
+#define RT_TUNE_INFLIGHT_DYNAMIC 33 /* 1 (default): with RT_TUNE_FRAMES_IN_FLIGHT > 1 and RT_TUNE_CHAIN_SPLIT 5,
+                                    ordered launches take dynamic wave tasks on a resident grid whatever the
+                                    one-in-flight trials chose (the next frame's blocks then fill the slots the
+                                    previous frame's tail frees; block dispatch runs two frames side by side
+                                    from their first blocks: C4 0.39 -> 0.36 ms per frame); 0: the trials'
+                                    distribution. Placement only */
 #define RT_TUNE_TOP_NODES 13     /* retired in r03 (0-85 accepted, no effect): an LDS copy of the four-wide
                                     tree's top levels; with float node rows loaded from global memory it
                                     measured slower (flat loads, 64-bit addresses) */

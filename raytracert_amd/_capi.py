@@ -49,6 +49,7 @@ TUNE_SPLIT_EIGHTH, TUNE_PRIORITY_BATCHES, TUNE_PIXEL_ORDER, TUNE_DYN_GROUP = 26,
 TUNE_SHADOW_HELPERS = 30
 TUNE_FRAMES_IN_FLIGHT = 31
 TUNE_ADOPT_ORDER = 32
+TUNE_INFLIGHT_DYNAMIC = 33
 BVH_INFO_FIELDS = 7
 STOCHASTIC = 1 << 8
 DEFAULT_SEED = 0x5EED

@@ -1516,17 +1516,34 @@ constexpr int kChainSteps = 256;   // max_lvl <= 254
 // they take the owner's hit by lane shuffles and walk lights r, r + roles, ... while the owner walks
 // lights 0, roles, ...; the owner ORs their verdicts into its mask and shades. Each light's walk is
 // the same walk on the same ray whichever lane runs it, so the mask is the same bits.
+// RT_LDS_PARK (A/B build): the step's values that only shading needs (the ray, lvl, the sample) wait
+// in LDS ([word][lane] beside the traversal stack) while the walks run, so they hold no VGPRs there.
+#ifndef RT_LDS_PARK
+#define RT_LDS_PARK 0
+#endif
+constexpr int kParkWords = 8;   // words per lane of the park area: ray xyz, lvl, sample, pixel (k_chain)
+struct Park {
+    float *base;   // [kParkWords][kBvhBlock] in LDS, or null
+    __device__ __forceinline__ void put(int k, float v) const { base[k * kBvhBlock + static_cast<int>(threadIdx.x)] = v; }
+    __device__ __forceinline__ float get(int k) const { return base[k * kBvhBlock + static_cast<int>(threadIdx.x)]; }
+};
+
 template <bool kAnyHit, int W, bool kCount, bool kInLane = false, bool kSteal = false>
 __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeParams &p, const DevWork &w, int step,
                                                 int sample, V3 org, V3 dst, int lvl, const LaneStack &stack, int *s_sh,
                                                 WorkTally<kCount> &wc, WorkTally<kCount> &ws, int role = 0, int roles = 1,
-                                                int plen = kWave) {
+                                                int plen = kWave, Park park = Park{nullptr}) {
     Secondary none;
     none.state = kChildNone;
     none.local = mk(0, 0, 0);   // trace() miss: black (:389-391)
     int bidx = -1;
     V3 bI = mk(0, 0, 0);
-    bvh_query_w<false, W, kSteal>(sc, org, sub(dst, org), role == 0, bidx, bI, stack, wc.tests, wc.visits);
+    V3 ray = sub(dst, org);
+    if (RT_LDS_PARK && park.base) {
+        park.put(0, ray.x); park.put(1, ray.y); park.put(2, ray.z);
+        park.put(3, as_float(lvl)); park.put(4, as_float(sample));
+    }
+    bvh_query_w<false, W, kSteal>(sc, org, ray, role == 0, bidx, bI, stack, wc.tests, wc.visits);
     if (bidx >= sc.nt) { w.counters[kErrorSlot] = 1; bidx = -1; }
     const int lane = __lane_id();
     if (roles > 1) {   // helpers take their owner's hit (owner and helpers are all active here)
@@ -1557,7 +1574,12 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
         }
     }
     if (role != 0) return none;   // (a helper's return value is not used)
-    return shade_hit<kInLane>(sc, p, w, step, sample, sub(dst, org), lvl, bidx, bI, [&](int l) { return ((mask >> l) & 1u) != 0; });
+    if (RT_LDS_PARK && park.base) {
+        ray = mk(park.get(0), park.get(1), park.get(2));
+        lvl = as_int(park.get(3));
+        sample = as_int(park.get(4));
+    }
+    return shade_hit<kInLane>(sc, p, w, step, sample, ray, lvl, bidx, bI, [&](int l) { return ((mask >> l) & 1u) != 0; });
 }
 
 // The chain launch: steps first..max_lvl of every query, each lane carrying its own ray through
@@ -1591,6 +1613,12 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
     float *__restrict__ out_f32, int fuse_spp, int spb, int nbatch, const FrameGeom g, int split, int split8) {
     extern __shared__ int32_t lds_stack[];
     __shared__ int s_q[kChainSteps], s_sh[kChainSteps];
+#if RT_LDS_PARK
+    __shared__ float s_park[kParkWords * kBvhBlock];
+    const Park park{s_park};
+#else
+    const Park park{nullptr};
+#endif
     for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) { s_q[i] = 0; s_sh[i] = 0; }
     __syncthreads();
     const LaneStack stack = lane_stack(sc, lds_stack);
@@ -1677,7 +1705,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         for (int step = first; step < kChainSteps; ++step) {
             if (step > first && role == 0) atomicAdd(&s_q[step], 1);
             const Secondary sec = chain_step<kAnyHit, W, kCount, kInLane, kSteal>(sc, p, w, step, sample, org, dst, lvl, stack,
-                                                                                  s_sh, wc, ws, role, roles, plen);
+                                                                                  s_sh, wc, ws, role, roles, plen, park);
             bool cont = sec.state == kChildTrace;
             if (roles > 1) cont = __shfl(static_cast<int>(cont), role ? lane - role * plen : lane) != 0;   // the owner's
             if (role) {

@@ -28,12 +28,24 @@ with tempfile.TemporaryDirectory() as d:
     for rnd in range(2):
         for v in variants:
             with R.Scene.load(path, device=0) as sc:
+                prio, FF = False, 2
                 for kv in filter(None, v.split(",")):
                     k, val = kv.split("=")
+                    if k == "prio":   # frames in flight on a high- and a low-priority stream
+                        prio = bool(int(val))
+                        continue
+                    if k == "F":      # frames in flight of the in-flight loop (default 2)
+                        FF = int(val)
+                        continue
                     sc.tune(k, int(val))
                 main = torch.cuda.current_stream(dev)
-                streams = [main, torch.cuda.Stream(dev)]
-                bufs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(2)]
+                if prio:
+                    lo, hi = torch.cuda.Stream.priority_range()
+                    streams = [torch.cuda.Stream(dev, priority=hi), torch.cuda.Stream(dev, priority=lo)]
+                    main = streams[0]
+                else:
+                    streams = [main] + [torch.cuda.Stream(dev) for _ in range(FF - 1)]
+                bufs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(max(2, FF))]
                 calib = 0
                 while calib < 64 and sc.trials()["choice"] < 0:
                     sc.render_frame_device(cp, 16, 16, bufs[0].data_ptr(), n, main.cuda_stream)
@@ -41,16 +53,16 @@ with tempfile.TemporaryDirectory() as d:
                     calib += 1
                 ref = bufs[0].clone()
                 res = []
-                for F in (2, 1):
+                for F in (FF, 1):
                     sc.tune("frames_in_flight", F)
                     for i in range(W * F):
-                        sc.render_frame_device(cp, 16, 16, bufs[i % 2].data_ptr(), n, streams[i % F].cuda_stream)
+                        sc.render_frame_device(cp, 16, 16, bufs[i % len(bufs)].data_ptr(), n, streams[i % F].cuda_stream)
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
                     for i in range(K):
-                        sc.render_frame_device(cp, 16, 16, bufs[i % 2].data_ptr(), n, streams[i % F].cuda_stream)
+                        sc.render_frame_device(cp, 16, 16, bufs[i % len(bufs)].data_ptr(), n, streams[i % F].cuda_stream)
                     torch.cuda.synchronize()
                     res.append((time.perf_counter() - t0) / K * 1e3)
                     assert all(torch.equal(b, ref) for b in bufs)
-                print(f"{wl_name} round {rnd} [{v or 'default'}] calib {calib}: 2 in flight {res[0]:.4f} ms, "
+                print(f"{wl_name} round {rnd} [{v or 'default'}] calib {calib}: {FF} in flight {res[0]:.4f} ms, "
                       f"1 in flight {res[1]:.4f} ms, trials {sc.trials()}", flush=True)
