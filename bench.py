@@ -716,14 +716,18 @@ def dropin_loop(obj, wl):
     # pf stays the reference's default 3 and max_lvl its 10 (the drop-in's globals); 'T' x2: the
     # first frame includes the upload of the workspace
     out = subprocess.run([exe, "keys", obj, str(wl["width"]), str(wl["height"]), os.path.join(d, "f"), "T", "T", "R",
-                          "P:2000"], check=True, capture_output=True, text=True, timeout=600).stdout.splitlines()
+                          "P:2000", "H", "H"], check=True, capture_output=True, text=True, timeout=600).stdout.splitlines()
     fr = [l.split() for l in out if l.startswith("frame ")]
     single = next(l.split() for l in out if l.startswith("single "))
+    floor = [float(l.split()[7]) for l in out if l.startswith("hostfloor ")]
     loop_ms = float(fr[1][10])
     n = wl["width"] * wl["height"] * wl["pf"] ** 2
     return {"what": "main.cpp:355-395 unchanged (performRayTracing per sub-sample) over the drop-in header, "
                     f"{wl['width']}x{wl['height']} pf {wl['pf']} = {n} calls",
             "loop_ms": loop_ms, "first_loop_ms": float(fr[0][10]), "render_image_ms": float(fr[2][7]),
+            "host_floor_ms": min(floor) if floor else None,
+            "host_floor_what": "the same loop with performRayTracing replaced by a function that only reads its "
+                               "arguments: the unchanged loop's own cost (two divisions and ~60 flops per call)",
             "single_call_us": float(single[4]), "single_calls": int(single[1]),
             "per_call_loop_estimate_s": round(float(single[4]) * n / 1e6, 1),
             "frames_equal": open(fr[1][1], "rb").read() == open(fr[2][1], "rb").read()}

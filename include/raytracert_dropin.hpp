@@ -530,22 +530,28 @@ struct TraceState {
             return false;
         return lights.empty() || std::memcmp(lights.data(), o.lights.data(), sizeof(Vec3Df) * lights.size()) == 0;
     }
-    bool matches_globals() const {   // the same test against the live globals, without copying them
-        if (scene != rtamd_dropin::scene() || gen != scene_generation() || amb != Ambient || dif != Diffuse ||
-            refl != Reflection || sha != Shadows || spec != Specular || refr != Refraction || pfx != pixelfactorX ||
-            pfy != pixelfactorY || w != WindowSize_X || h != WindowSize_Y || lvl != max_lvl ||
-            lights.size() != MyLightPositions.size() || !same_bits3(cam.p, MyCameraPosition.p))
-            return false;
-        for (size_t i = 0; i < lights.size(); ++i)
-            if (!same_bits3(lights[i].p, MyLightPositions[i].p)) return false;
-        return true;
+    // The same test against the live globals, without copying them: every comparison folded into one
+    // word (no branch per global: this runs once per performRayTracing call of the 'r' loop).
+    bool matches_globals() const {
+        uint32_t x = static_cast<uint32_t>(scene != rtamd_dropin::scene()) | static_cast<uint32_t>(gen != scene_generation()) |
+                     static_cast<uint32_t>(amb != Ambient) | static_cast<uint32_t>(dif != Diffuse) |
+                     static_cast<uint32_t>(refl != Reflection) | static_cast<uint32_t>(sha != Shadows) |
+                     static_cast<uint32_t>(spec != Specular) | static_cast<uint32_t>(refr != Refraction) |
+                     (pfx ^ pixelfactorX) | (pfy ^ pixelfactorY) | (w ^ WindowSize_X) | (h ^ WindowSize_Y) |
+                     static_cast<uint32_t>(lvl ^ max_lvl) | diff3(cam.p, MyCameraPosition.p);
+        const Vec3Df *a = lights.data(), *b = MyLightPositions.data();
+        const size_t nl = lights.size();
+        if (x != 0 || nl != MyLightPositions.size()) return false;
+        for (size_t i = 0; i < nl; ++i) x |= diff3(a[i].p, b[i].p);
+        return x == 0;
     }
-    static bool same_bits3(const float *a, const float *b) {
+    static uint32_t diff3(const float *a, const float *b) {   // 0 when the three floats are the same bits
         uint32_t u[3], v[3];
         std::memcpy(u, a, 12);
         std::memcpy(v, b, 12);
-        return ((u[0] ^ v[0]) | (u[1] ^ v[1]) | (u[2] ^ v[2])) == 0;
+        return (u[0] ^ v[0]) | (u[1] ^ v[1]) | (u[2] ^ v[2]);
     }
+    static bool same_bits3(const float *a, const float *b) { return diff3(a, b) == 0; }
 };
 
 inline bool same_bits(const Vec3Df &a, const Vec3Df &b) { return std::memcmp(a.p, b.p, sizeof a.p) == 0; }
@@ -629,14 +635,23 @@ inline bool start_frame(const Vec3Df &origin, const Vec3Df &dest) {
 
 // performRayTracing (raytracing.cpp:410-416). The sub-samples of an 'r' loop come from the frame
 // cache (see the top of this file); any other ray is traced on its own. Same colours either way.
-inline Vec3Df performRayTracing(const Vec3Df &origin, const Vec3Df &dest) {
+namespace rtamd_dropin {
+// performRayTracing's path for a call the frame cache does not answer (out of line: the cached
+// path below stays small enough to inline into the host's loop)
+__attribute__((noinline)) inline Vec3Df perform_uncached(const Vec3Df &origin, const Vec3Df &dest) {
 #ifndef RTAMD_DROPIN_NO_FRAME_CACHE
-    using namespace rtamd_dropin;
-    FrameCache &fc = frame_cache();
-    if (fc.next < fc.n && fc.matches(origin, dest) && fc.state.matches_globals()) return fc.take();
-    if (start_frame(origin, dest)) return fc.take();
+    if (start_frame(origin, dest)) return frame_cache().take();
 #endif
     return trace(origin, dest, 0);
+}
+}  // namespace rtamd_dropin
+
+inline Vec3Df performRayTracing(const Vec3Df &origin, const Vec3Df &dest) {
+#ifndef RTAMD_DROPIN_NO_FRAME_CACHE
+    rtamd_dropin::FrameCache &fc = rtamd_dropin::frame_cache();
+    if (__builtin_expect(fc.next < fc.n && fc.matches(origin, dest) && fc.state.matches_globals(), 1)) return fc.take();
+#endif
+    return rtamd_dropin::perform_uncached(origin, dest);
 }
 
 // the same for many rays in one GPU call

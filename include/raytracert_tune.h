@@ -100,11 +100,11 @@ extern "C" {
                                     already ordered starts from that pipeline's measured order (frames in
                                     flight); 0: it learns its own from a cold launch. Placement only */
 #define RT_TUNE_INFLIGHT_DYNAMIC 33 /* 1 (default): with RT_TUNE_FRAMES_IN_FLIGHT > 1 and RT_TUNE_CHAIN_SPLIT 5,
-                                    ordered launches take dynamic wave tasks on a resident grid whatever the
-                                    one-in-flight trials chose (the next frame's blocks then fill the slots the
-                                    previous frame's tail frees; block dispatch runs two frames side by side
-                                    from their first blocks: C4 0.39 -> 0.36 ms per frame); 0: the trials'
-                                    distribution. Placement only */
+                                    ordered launches take dynamic wave tasks on a resident grid when the
+                                    trials timed the chosen shape with them within 3% of the choice (the next
+                                    frame's blocks then fill the slots the previous frame's tail frees; block
+                                    dispatch runs two frames side by side from their first blocks: C4 0.387
+                                    -> 0.377 ms per frame); 0: always the trials' distribution. Placement only */
 #define RT_TUNE_TOP_NODES 13     /* retired in r03 (0-85 accepted, no effect): an LDS copy of the four-wide
                                     tree's top levels; with float node rows loaded from global memory it
                                     measured slower (flat loads, 64-bit addresses) */
@@ -137,12 +137,12 @@ int rt_diag_read(rt_scene *scene, int64_t offset, int64_t count, uint64_t *out);
 /* The per-view launch trials of render pipeline 0 (RT_TUNE_WAVE_STEAL 2 x RT_TUNE_CHAIN_SPLIT 5 x
  * RT_TUNE_SHADOW_HELPERS 2 x RT_TUNE_STEAL_QUARTER -1): info = {candidates timed (0 while pending),
  * chosen candidate (-1 pending), its wave_steal, its chain distribution, its shadow helpers, its
- * quarter tier}; trial_ms (may be NULL) = each candidate's chain-launch time. Candidates, per
+ * quarter tier, its distribution with frames in flight (RT_TUNE_INFLIGHT_DYNAMIC)}; trial_ms (may be NULL) = each candidate's chain-launch time. Candidates, per
  * distribution (0, then 4): the plain kernel (without, then with shadow helpers), then the stealing
  * kernel, each at distribution 0 also with the quarter tier. After a warm-up launch each is timed
  * twice (two rounds) and its faster launch counts; the fastest candidate is kept unless within 2% of
  * candidate 0. Frames in flight: the other pipelines adopt pipeline 0's decision. Placement only. */
-#define RT_TRIAL_INFO_FIELDS 6
+#define RT_TRIAL_INFO_FIELDS 7
 #define RT_MAX_TRIALS 10
 int rt_scene_trials(rt_scene *scene, int32_t info[RT_TRIAL_INFO_FIELDS], float trial_ms[RT_MAX_TRIALS]);
 

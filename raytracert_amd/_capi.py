@@ -27,7 +27,7 @@ COMM_ID_BYTES = 128
 RT_HOST_ONLY = -1
 RT_MAX_LIGHTS = 16        # lights held inline in rt_params; more through rt_params.light_list
 RT_LIGHTS_LIMIT = 65536
-RT_TRIAL_INFO_FIELDS, RT_MAX_TRIALS = 6, 10
+RT_TRIAL_INFO_FIELDS, RT_MAX_TRIALS = 7, 10
 SAMPLES_RGB, SAMPLES_RAY_RGB = 3, 9   # rt_trace_frame_samples record layouts
 RT_WS_ARRAYS = 20   # rt_workspace_layout arrays
 

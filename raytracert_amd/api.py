@@ -310,7 +310,7 @@ class Scene:
         check(lib().rt_scene_trials(self._h, info.ctypes.data, ms.ctypes.data))
         n = int(info[0])
         return {"trials": n, "choice": int(info[1]), "wave_steal": int(info[2]), "chain_split": int(info[3]),
-                "shadow_helpers": int(info[4]), "steal_quarter": int(info[5]),
+                "shadow_helpers": int(info[4]), "steal_quarter": int(info[5]), "inflight_split": int(info[6]),
                 "trial_ms": [round(float(x), 4) for x in ms[:n]]}
 
     def batch_durations(self) -> np.ndarray:

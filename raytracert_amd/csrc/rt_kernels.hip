@@ -1521,6 +1521,7 @@ constexpr int kChainSteps = 256;   // max_lvl <= 254
 #ifndef RT_LDS_PARK
 #define RT_LDS_PARK 0
 #endif
+
 constexpr int kParkWords = 8;   // words per lane of the park area: ray xyz, lvl, sample, pixel (k_chain)
 struct Park {
     float *base;   // [kParkWords][kBvhBlock] in LDS, or null
@@ -1642,6 +1643,8 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
     const bool dyn = kInLane && sc.chain_split == 4;
     drive_queries((nbatch + extra) * kWave, dyn ? 4 : (sc.chain_split & 3), dyn ? &w.counters[kWaveQueueSlot] : w.wq + (2 * first) * kWqSlot,
                   [&](int j0, int vend) {
+        const FrameGeom &gl = g;
+        const ShadeParams &pl = p;
         const int vb = j0 >> 6;   // this wave's virtual batch (wave-uniform for the orderable distributions)
         // split tiers of the order: 8 parts, then 4, then 2; part = which part of batch order[ob]
         int ob = vb - (ordered ? extra : 0), nparts = 1, part = 0;
@@ -1667,8 +1670,8 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         int px = -1;   // (out_mode 2: the sample's output slot, pixel x spp + sub-sample)
         // shadow helpers (RT_TUNE_SHADOW_HELPERS): in a split wave of the fused launch the lanes past
         // the part's plen samples help their owners' shadow walks, roles = lanes per sample (<= lights)
-        const int roles = (kInLane && !kSteal && nparts > 1 && sc.shadow_helpers && (p.flags & RT_SHADOWS))
-                              ? max(1, min(kWave / plen, p.n_lights)) : 1;
+        const int roles = (kInLane && !kSteal && nparts > 1 && sc.shadow_helpers && (pl.flags & RT_SHADOWS))
+                              ? max(1, min(kWave / plen, pl.n_lights)) : 1;
         const int role = (roles > 1 && lane >= plen && lane < roles * plen) ? lane / plen : 0;
         [&]() {
         bool own = lane_on && j < nq;
@@ -1677,8 +1680,8 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         if (kInLane) {   // sample j: its primary ray, as k_gen_primary makes it
             int64_t pxi = 0;
             int sub = 0;
-            if (own && !primary_sample(g, j, org, dst, pxi, sub)) {
-                if (g.out_mode == 0 && out_u8 && sub == 0) { out_u8[3 * pxi] = 0; out_u8[3 * pxi + 1] = 0; out_u8[3 * pxi + 2] = 0; }
+            if (own && !primary_sample(gl, j, org, dst, pxi, sub)) {
+                if (gl.out_mode == 0 && out_u8 && sub == 0) { out_u8[3 * pxi] = 0; out_u8[3 * pxi + 1] = 0; out_u8[3 * pxi + 2] = 0; }
                 own = false;
             }
             if (roles > 1) {   // a helper follows its owner's sample (all lanes are still here)
@@ -1686,8 +1689,8 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
                 if (role) own = o;
             }
             if (!own || (role == 0 && !lane_on)) return;
-            if (role == 0) px = g.out_mode == 2 ? static_cast<int>(pxi) * fuse_spp + sub : static_cast<int>(pxi);
-            if (g.out_mode == 2 && g.sample_stride == 9 && role == 0) {   // the record's ray (RT_SAMPLES_RAY_RGB)
+            if (role == 0) px = gl.out_mode == 2 ? static_cast<int>(pxi) * fuse_spp + sub : static_cast<int>(pxi);
+            if (gl.out_mode == 2 && gl.sample_stride == 9 && role == 0) {   // the record's ray (RT_SAMPLES_RAY_RGB)
                 float *r = out_f32 + 9 * static_cast<int64_t>(px);
                 r[0] = org.x; r[1] = org.y; r[2] = org.z; r[3] = dst.x; r[4] = dst.y; r[5] = dst.z;
             }
@@ -1704,7 +1707,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         }
         for (int step = first; step < kChainSteps; ++step) {
             if (step > first && role == 0) atomicAdd(&s_q[step], 1);
-            const Secondary sec = chain_step<kAnyHit, W, kCount, kInLane, kSteal>(sc, p, w, step, sample, org, dst, lvl, stack,
+            const Secondary sec = chain_step<kAnyHit, W, kCount, kInLane, kSteal>(sc, pl, w, step, sample, org, dst, lvl, stack,
                                                                                   s_sh, wc, ws, role, roles, plen, park);
             bool cont = sec.state == kChildTrace;
             if (roles > 1) cont = __shfl(static_cast<int>(cont), role ? lane - role * plen : lane) != 0;   // the owner's
@@ -1723,9 +1726,9 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
             lvl = sec.lvl;
         }
         }();
-        if (kInLane && g.out_mode == 2) {   // every sub-sample's own colour (rt_trace_frame_samples)
+        if (kInLane && gl.out_mode == 2) {   // every sub-sample's own colour (rt_trace_frame_samples)
             if (px >= 0) {
-                float *o = out_f32 + static_cast<int64_t>(g.sample_stride) * px + (g.sample_stride - 3);
+                float *o = out_f32 + static_cast<int64_t>(gl.sample_stride) * px + (gl.sample_stride - 3);
                 o[0] = rgb.x; o[1] = rgb.y; o[2] = rgb.z;
             }
         } else if (kInLane) {   // k_frame's arithmetic: a pixel's fuse_spp sub-samples sit in adjacent lanes

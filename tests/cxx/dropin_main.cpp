@@ -11,8 +11,8 @@
 //   dropin_main host <obj>                                    loader, MyMesh, normals, getMaterial
 //   dropin_main keys <obj> W H <prefix> <key> [<key> ...]     a key session; 'r' writes <prefix>N.ppm
 // A key is one character; 'd@X,Y' is 'd' with the mouse at (X, Y); 'R' renders through the one-call
-// renderImage() for comparison; 'T' times the 'r' loop, 'P:N' N single performRayTracing calls on
-// rays the frame cache has never seen.
+// renderImage() for comparison; 'T' times the 'r' loop, 'H' the same loop with no trace at all (the
+// host floor), 'P:N' N single performRayTracing calls on rays the frame cache has never seen.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -144,6 +144,39 @@ static void render_r(bool timed) {
                 Diffuse, Specular, Reflection, Shadows, Refraction, MyLightPositions.size(), timed ? 1e3 * (t1 - t0) : 0.0);
 }
 
+// The host floor of the 'r' loop: the same loop with performRayTracing replaced by a function that
+// only reads its arguments (no GPU, no cache lookup): what the unchanged loop costs by itself.
+static Vec3Df host_only_trace(const Vec3Df &o, const Vec3Df &d) { return Vec3Df(o[0] * 1e-9f, d[1] * 1e-9f, 0.5f); }
+static void render_host_floor() {
+    const double t0 = now_s();
+    Vec3Df origin00, dest00, origin01, dest01, origin10, dest10, origin11, dest11, origin, dest;
+    produceRay(0, 0, &origin00, &dest00);
+    produceRay(0, WindowSize_Y - 1, &origin01, &dest01);
+    produceRay(WindowSize_X - 1, 0, &origin10, &dest10);
+    produceRay(WindowSize_X - 1, WindowSize_Y - 1, &origin11, &dest11);
+    float divX = (WindowSize_X * pixelfactorX - 1);
+    float divY = (WindowSize_Y * pixelfactorY - 1);
+    int raysPerPixel = (pixelfactorX * pixelfactorY);
+    Vec3Df acc(0, 0, 0);
+    for (unsigned int y = 0; y < WindowSize_Y; ++y)
+        for (unsigned int x = 0; x < WindowSize_X; ++x) {
+            Vec3Df rgb = Vec3Df(0, 0, 0);
+            for (int subx = 0; subx < (int)pixelfactorX; subx++)
+                for (int suby = 0; suby < (int)pixelfactorY; suby++) {
+                    float xscale = 1.0f - (float(x) * pixelfactorX + subx) / divX;
+                    float yscale = 1.0f - (float(y) * pixelfactorY + suby) / divY;
+                    origin = yscale * (xscale * origin00 + (1 - xscale) * origin10) +
+                             (1 - yscale) * (xscale * origin01 + (1 - xscale) * origin11);
+                    dest = yscale * (xscale * dest00 + (1 - xscale) * dest10) +
+                           (1 - yscale) * (xscale * dest01 + (1 - xscale) * dest11);
+                    rgb += host_only_trace(origin, dest);
+                }
+            acc += rgb / raysPerPixel;
+        }
+    std::printf("hostfloor %u x %u pf %u ms %.3f (checksum %g)\n", WindowSize_X, WindowSize_Y, pixelfactorX,
+                1e3 * (now_s() - t0), acc[0] + acc[1] + acc[2]);
+}
+
 // the same frame through renderImage (one call), written like the loop's Image
 static void render_one_call() {
     Vec3Df c[8];
@@ -231,6 +264,8 @@ int main(int argc, char **argv) {
             render_one_call();
         } else if (k[0] == 'T') {
             render_r(true);
+        } else if (k[0] == 'H') {
+            render_host_floor();
         } else if (k[0] == 'P' && k[1] == ':') {   // single calls off the frame cache (rays of no frame)
             const int n = std::atoi(k + 2);
             Vec3Df o00, d00, o11, d11, acc;
