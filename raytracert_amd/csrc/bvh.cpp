@@ -16,7 +16,8 @@
 //    SPATIAL displacement that any of the three tests can absorb by K eps |w| with
 //    K = 36/c + 18/c^1.5 + 2/sqrt(c). A point at distance d outside the triangle has |w| <= 2L + d
 //    (L = longest of |u|, |v|), so it can only be accepted if d <= 2 K eps L / (1 - K eps). The
-//    box is the triangle's bounding box widened by 4x that bound plus 1e-7 L.
+//    box is the triangle's bounding box widened by 4x that bound, taken in the plane (axis k:
+//    times sqrt(1 - n_k^2), r04), plus 1e-7 L.
 //  * Off-plane. I = o + r*dir with r = a/b rounded; whatever the error in r, I stays on the ray, and
 //    its distance from the plane is at most ~6 eps (|o - T0| + |I - o|). The kernel adds
 //    pad_ray = 64 eps (|o|_1 + M_1) to every box at traversal time (M_1 = max |x|+|y|+|z| of the
@@ -421,12 +422,27 @@ bool acceptance_box(const TriRec &T, const float *v0, const float *v1, const flo
     const double K = 36.0 / c + 18.0 / (c * std::sqrt(c)) + 2.0 / std::sqrt(c);
     const double ke = K * kEps;
     if (!(ke <= kMaxDelta)) return false;
-    const double pad = 4.0 * 2.0 * ke * L / (1.0 - ke) + 1e-7 * L;
+    const double pad = 4.0 * 2.0 * ke * L / (1.0 - ke);
+    // The displacement is in the plane (the off-plane part is the per-ray pad's): along axis k a
+    // disc of radius pad in the plane reaches pad * sqrt(1 - n_k^2). The normal is the double cross
+    // product of the exact float edges (error ~1e-16 / sin(angle) <= ~1e-14 here); the 1e-12 under
+    // the root keeps every axis >= 1e-6 of the pad, far above that.
+    double e1[3], e2[3], nd[3];
     for (int k = 0; k < 3; ++k) {
+        e1[k] = double(v1[k]) - double(v0[k]);
+        e2[k] = double(v2[k]) - double(v0[k]);
+    }
+    nd[0] = e1[1] * e2[2] - e1[2] * e2[1];
+    nd[1] = e1[2] * e2[0] - e1[0] * e2[2];
+    nd[2] = e1[0] * e2[1] - e1[1] * e2[0];
+    const double n2 = nd[0] * nd[0] + nd[1] * nd[1] + nd[2] * nd[2];
+    for (int k = 0; k < 3; ++k) {
+        const double along = n2 > 0 ? std::min(1.0, std::sqrt(std::max(0.0, 1.0 - nd[k] * nd[k] / n2) + 1e-12)) : 1.0;
+        const double pk = pad * along + 1e-7 * L;
         const double mn = std::min({double(v0[k]), double(v1[k]), double(v2[k])});
         const double mx = std::max({double(v0[k]), double(v1[k]), double(v2[k])});
-        lo[k] = down(mn - pad);
-        hi[k] = up(mx + pad);
+        lo[k] = down(mn - pk);
+        hi[k] = up(mx + pk);
     }
     return true;
 }

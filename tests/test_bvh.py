@@ -191,3 +191,37 @@ def test_acceptance_claim_on_near_threshold_slivers():
             n_box += st == 0
             accepted += n
     assert n_box >= 60 and accepted > 3000
+
+
+def test_acceptance_claim_with_in_plane_pads_on_axis_aligned_slivers():
+    """The acceptance pad is an in-plane displacement, so the box widens axis k by the pad times
+    sqrt(1 - n_k^2) (r04): a triangle in an axis plane gets (almost) no pad along that axis, and
+    the off-plane error of I is the per-ray pad's alone. Slivers of 0.95-2.2 degrees (the largest
+    pads) in the three axis planes, exactly and tilted by 1e-6 to 1e-2 rad, with rays aimed at
+    their edges, grazing and from far away, against the oracle's arithmetic; and the box along
+    the normal axis stays far thinner than in the plane."""
+    rng = np.random.default_rng(31)
+    n_box = accepted = 0
+    for i in range(48):
+        axis = i % 3
+        theta = np.deg2rad(rng.uniform(0.95, 2.2))
+        L = 10 ** rng.uniform(-2, 2)
+        base = rng.normal(size=3) * 10 ** rng.uniform(-1, 2)
+        ax = [k for k in range(3) if k != axis]
+        e1 = np.zeros(3); e2 = np.zeros(3)
+        phi = rng.uniform(0, 2 * np.pi)
+        e1[ax[0]], e1[ax[1]] = np.cos(phi), np.sin(phi)
+        e2[ax[0]], e2[ax[1]] = -np.sin(phi), np.cos(phi)
+        tilt = 0.0 if i % 2 == 0 else 10 ** rng.uniform(-6, -2)
+        e2[axis] = np.sin(tilt); e2 /= np.linalg.norm(e2)
+        la, lb = L, L * rng.uniform(0.3, 1.0)
+        T = np.stack([base, base + la * e1, base + lb * (np.cos(theta) * e1 + np.sin(theta) * e2)]).astype(np.float32)
+        for far in (False, True):
+            st, n = _check_triangle(T, _rays_near(T, rng, 6000, far=far))
+            n_box += st == 0
+            accepted += n
+        st, lo, hi = bvh_acceptance_box(T)
+        if st == 0 and tilt == 0.0:
+            ext = np.asarray(hi, np.float64) - np.asarray(lo, np.float64)
+            assert ext[axis] < 1e-3 * ext[ax].max(), (ext, axis)
+    assert n_box >= 80 and accepted > 3000
