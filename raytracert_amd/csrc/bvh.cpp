@@ -23,8 +23,8 @@
 //    pad_ray = 64 eps (|o|_1 + M_1) to every box at traversal time (M_1 = max |x|+|y|+|z| of the
 //    vertices), which also covers the rounding of I itself.
 //  * Triangles with D == 0 or non-finite (then s, t are NaN/inf and the reference accepts almost
-//    anything), or with K eps > 0.2 (angle at T0 below ~1 degree; there the first-order bound's
-//    second-order terms, ~(K eps)^2, stay far inside the factor-4 pad), are not put in the tree:
+//    anything), or with K eps > kMaxDelta = 0.2 (angle at T0 below ~1 degree; up to there the
+//    first-order bound's second-order terms, ~(K eps)^2, stay far inside the factor-4 pad), are not put in the tree:
 //    every query tests them first (the "always" list). Triangles with n == 0 are rejected by
 //    isNullVector and never tested.
 //  * Box tests and the distance cull use relative slack (1e-5) far above their rounding error.
@@ -49,13 +49,23 @@ namespace rt {
 namespace {
 
 constexpr double kEps = 5.9604644775390625e-08;   // 2^-24
-constexpr double kMaxDelta = 0.2;    // K*eps bound for a tree triangle (pad <= 2 L): angle at T0 >~ 1 degree
+#ifndef RT_BVH_MAX_KE
+#define RT_BVH_MAX_KE 0.2
+#endif
+// K*eps bound for a tree triangle (pad <= 2 L): angle at T0 >~ 1 degree. 0.5 (pad <= 8 L, >~ 0.75
+// degree; its neglected terms still inside the factor-4 pad, tests/test_bvh.py) moved 13 of the car
+// model's 30 always-tested slivers into the tree: ref_default 0.249 -> 0.235 ms but C2 0.079 ->
+// 0.087 ms (their big boxes lengthen the car region's walks; profiles/r04_ab_max_ke.txt).
+constexpr double kMaxDelta = RT_BVH_MAX_KE;
 constexpr int kBins = 16;
 #ifndef RT_BVH_MAX_LEAF
 #define RT_BVH_MAX_LEAF 2   // measured: 2 beats 4 by ~4% (C4 and the 1M-triangle grid), 8 loses 15%
 #endif
 #ifndef RT_BVH_TRAV_COST
 #define RT_BVH_TRAV_COST 1.0
+#endif
+#ifndef RT_BVH_INPLANE_PAD
+#define RT_BVH_INPLANE_PAD 1   // the acceptance pad in the triangle's plane only (0: on every axis, r03)
 #endif
 constexpr int kMaxLeaf = RT_BVH_MAX_LEAF;
 constexpr double kTravCost = RT_BVH_TRAV_COST;   // SAH: node traversal relative to one triangle test
@@ -437,7 +447,7 @@ bool acceptance_box(const TriRec &T, const float *v0, const float *v1, const flo
     nd[2] = e1[0] * e2[1] - e1[1] * e2[0];
     const double n2 = nd[0] * nd[0] + nd[1] * nd[1] + nd[2] * nd[2];
     for (int k = 0; k < 3; ++k) {
-        const double along = n2 > 0 ? std::min(1.0, std::sqrt(std::max(0.0, 1.0 - nd[k] * nd[k] / n2) + 1e-12)) : 1.0;
+        const double along = !RT_BVH_INPLANE_PAD ? 1.0 : n2 > 0 ? std::min(1.0, std::sqrt(std::max(0.0, 1.0 - nd[k] * nd[k] / n2) + 1e-12)) : 1.0;
         const double pk = pad * along + 1e-7 * L;
         const double mn = std::min({double(v0[k]), double(v1[k]), double(v2[k])});
         const double mx = std::max({double(v0[k]), double(v1[k]), double(v2[k])});

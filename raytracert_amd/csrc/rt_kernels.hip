@@ -138,7 +138,10 @@ __device__ __forceinline__ void sgpr_fence(const TriRec &T) {
 // One rayIntersectTriangle + intersectMesh update (raytracing.cpp:106-154, :180-187). In index
 // order the update is the reference's strict '<' (:183); out of order (kLex, the BVH) it is the
 // equivalent lexicographic (distance, index) minimum.
-template <bool kAnyHit, bool kLex = false>
+// kSignFirst: reject r = a / b < 0 from the signs of a and b before the division (exact: with
+// |a| > 2^-100 |b| the quotient cannot round to -0, the one negative-signed value :125 lets through),
+// so a wave whose lanes all face away from the plane skips the correctly rounded division.
+template <bool kAnyHit, bool kLex = false, bool kSignFirst = false>
 __device__ __forceinline__ void test_triangle(const TriRec &T, int t, V3 o, V3 dir, float &best, int &bidx, V3 &bI,
                                               bool &done) {
     if (kAnyHit && done) return;
@@ -146,6 +149,7 @@ __device__ __forceinline__ void test_triangle(const TriRec &T, int t, V3 o, V3 d
     const float b = T.n[0] * dir.x + T.n[1] * dir.y + T.n[2] * dir.z;          // :113
     const float a = -(T.n[0] * w0.x + T.n[1] * w0.y + T.n[2] * w0.z);          // :114
     if (fabsf(b) < 0.00001f) return;                                            // :115
+    if (kSignFirst && (a < 0.0f) != (b < 0.0f) && fabsf(a) > fabsf(b) * 0x1p-100f) return;   // r < 0 (:125)
     const float r = a / b;                                                      // :124
     if (r < 0) return;                                                          // :125
     const V3 I = mk(o.x + dir.x * r, o.y + dir.y * r, o.z + dir.z * r);         // :130
@@ -236,6 +240,19 @@ struct LaneStack {
         if (sp >= cap) v = ovf[static_cast<size_t>(sp - cap) * stride + gl];
         return v;
     }
+    // The entry below sp if sp > base, else none (sp unchanged). When every active lane's entry is
+    // in LDS (a wave-uniform test) it is one ds_read; else pop's two reads, which the compiler
+    // merges into a flat load through a pointer select (r04: the walk's postponement and leaf-loop
+    // pops used that flat form every time).
+    __device__ __forceinline__ int32_t pop_or(int &sp, int base, int32_t none) const {
+        if (__all(sp <= cap)) {
+            const int32_t v = lds[max(sp - 1, 0) * width + static_cast<int>(threadIdx.x)];
+            const int32_t r = sp > base ? v : none;
+            sp = max(sp - 1, base);
+            return r;
+        }
+        return sp > base ? pop(sp) : none;
+    }
 };
 
 // Dynamic LDS of the per-lane BVH kernels: [lds_stack entries][block lanes] of stack.
@@ -286,6 +303,12 @@ __device__ __forceinline__ bool box_hit(const RayBox &R, float lx, float ly, flo
 // The always list (ill-conditioned triangles, bvh.cpp): every query tests them. Their records are
 // gathered contiguously (always_recs) and streamed like the brute-force loop: wave-uniform,
 // two records alternating so one load is in flight behind the arithmetic.
+#ifndef RT_LEAF_SIGN
+#define RT_LEAF_SIGN 0     // the same in the walks' leaf loops
+#endif
+#ifndef RT_ALWAYS_SIGN
+#define RT_ALWAYS_SIGN 1   // the always-tested list (uniform records, coherent rays) rejects r < 0 by signs first
+#endif
 template <bool kAnyHit>
 __device__ __forceinline__ void test_always(const DevScene &sc, V3 o, V3 dir, float &best, int &bidx, V3 &bI,
                                             bool &done) {
@@ -298,14 +321,14 @@ __device__ __forceinline__ void test_always(const DevScene &sc, V3 o, V3 dir, fl
         if (kAnyHit && (i & 15) == 0 && __all(done)) return;
         sgpr_fence(A);
         const TriRec B = recs[i + 1];
-        test_triangle<kAnyHit, true>(A, static_cast<int>(sc.always[i]), o, dir, best, bidx, bI, done);
+        test_triangle<kAnyHit, true, RT_ALWAYS_SIGN>(A, static_cast<int>(sc.always[i]), o, dir, best, bidx, bI, done);
         sgpr_fence(B);
         A = recs[min(i + 2, n - 1)];
-        test_triangle<kAnyHit, true>(B, static_cast<int>(sc.always[i + 1]), o, dir, best, bidx, bI, done);
+        test_triangle<kAnyHit, true, RT_ALWAYS_SIGN>(B, static_cast<int>(sc.always[i + 1]), o, dir, best, bidx, bI, done);
     }
     if (i < n) {
         sgpr_fence(A);
-        test_triangle<kAnyHit, true>(A, static_cast<int>(sc.always[i]), o, dir, best, bidx, bI, done);
+        test_triangle<kAnyHit, true, RT_ALWAYS_SIGN>(A, static_cast<int>(sc.always[i]), o, dir, best, bidx, bI, done);
     }
 }
 
@@ -419,12 +442,37 @@ constexpr int32_t kDoneRef = kBvhEmpty;   // "no ref": a count-0 leaf is never a
 // for the plane's float bound b (Bvh4F), instead of (b -/+ pad - o) * inv: the same value up to a few
 // ulps of (|o| + pad) * |inv| and of |t|, inside the pad (64 ulps of |o| + the scene's extent) and the
 // 1e-5 relative slack of the te <= tx test.
+//
+// The six planes of two children are one v_pk_fma_f32 each (r04): a row's float4 is two register
+// pairs, and op_sel / op_sel_hi broadcast one half of a per-ray pair to both elements, so the
+// per-ray constants live in five pairs with no splat copies. Per element the packed FMA is the
+// same IEEE fused multiply-add as v_fma_f32 (same rounding and denormal mode), so every slab
+// parameter has the bits of the scalar form.
+#ifndef RT_PK_BOX
+#define RT_PK_BOX 0   // measured: VALU -5% but C4 +1-2% (profiles/r04_ab_pk_box.txt); kept for the record
+#endif
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pk_fma_xy(f2 a, f2 s) {          // a * s.x + s.y, both elements
+    f2 d;
+    asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(d) : "v"(a), "v"(s));
+    return d;
+}
+__device__ __forceinline__ f2 pk_fma_x_x(f2 a, f2 s, f2 t) {   // a * s.x + t.x
+    f2 d;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[1,0,0]" : "=v"(d) : "v"(a), "v"(s), "v"(t));
+    return d;
+}
+__device__ __forceinline__ f2 pk_fma_x_y(f2 a, f2 s, f2 t) {   // a * s.x + t.y
+    f2 d;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(d) : "v"(a), "v"(s), "v"(t));
+    return d;
+}
 struct Ray4 {
-    V3 o, inv;
-    float tcull;
-    float bnx, bny, bnz, bfx, bfy, bfz;   // (+/-pad - o) * inv per axis, near and far plane
-    float inv_dlen;                       // an upper bound of 1.00001 / |dir|
-    uint32_t rows[6];                     // byte offsets in a Bvh4F of the near rows (x, y, z), then the far rows
+    f2 ax, ay, az;   // per axis (inv, (+/-pad - o) * inv of the near plane)
+    f2 fxy;          // (+/-pad - o) * inv of the far planes x, y
+    f2 fzc;          // (far plane z, tcull)
+    float inv_dlen;  // an upper bound of 1.00001 / |dir|
+    uint32_t rows[6];   // byte offsets in a Bvh4F of the near rows (x, y, z), then the far rows
 };
 
 // tcull for the current best: no child whose entry parameter exceeds it can hold a hit at
@@ -439,28 +487,54 @@ __device__ __forceinline__ float cull_param(const Ray4 &R, float best, float pad
 template <bool kAnyHit>
 __device__ __forceinline__ int32_t node4_next(const Ray4 &R, const Node4Rows &nd, const LaneStack &stack, int &sp,
                                               int base = 0) {
-    const V3 inv = R.inv;
-    const float nx[4] = {nd.n[0].x, nd.n[0].y, nd.n[0].z, nd.n[0].w}, fx[4] = {nd.f[0].x, nd.f[0].y, nd.f[0].z, nd.f[0].w};
-    const float ny[4] = {nd.n[1].x, nd.n[1].y, nd.n[1].z, nd.n[1].w}, fy[4] = {nd.f[1].x, nd.f[1].y, nd.f[1].z, nd.f[1].w};
-    const float nz[4] = {nd.n[2].x, nd.n[2].y, nd.n[2].z, nd.n[2].w}, fz[4] = {nd.f[2].x, nd.f[2].y, nd.f[2].z, nd.f[2].w};
+    // te <= tx (1 + 1e-5) and, closest-hit, te <= tcull, as one compare against their minimum.
+    // te is finite for every non-empty child (bounds and inv are finite and |b inv| < 2^120, so no
+    // FMA overflows; an empty slot's +inf/-inf bounds give te = +inf > tx = -inf), so a wanted
+    // child's key is below INFINITY, which marks the others
+    // (against two compares and an integer min of te: C4 0.418 -> 0.415 ms, C5 6.75 -> 6.71, C3
+    // 0.254 -> 0.247; profiles/r03_ab_node_lim.txt)
+    const float tcull = R.fzc.y;
     int32_t rc[4] = {nd.ref.x, nd.ref.y, nd.ref.z, nd.ref.w};
     float tc[4];
+#if RT_PK_BOX
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const float tnx = fmaf(nx[k], inv.x, R.bnx), tfx = fmaf(fx[k], inv.x, R.bfx);
-        const float tny = fmaf(ny[k], inv.y, R.bny), tfy = fmaf(fy[k], inv.y, R.bfy);
-        const float tnz = fmaf(nz[k], inv.z, R.bnz), tfz = fmaf(fz[k], inv.z, R.bfz);
-        const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
-        const float tx = fminf(fminf(tfx, tfy), tfz);
-        // te <= tx (1 + 1e-5) and, closest-hit, te <= tcull, as one compare against their minimum.
-        // te is finite for every non-empty child (bounds and inv are finite and |b inv| < 2^120, so no
-        // FMA overflows; an empty slot's +inf/-inf bounds give te = +inf > tx = -inf), so a wanted
-        // child's key is below INFINITY, which marks the others
-        // (against two compares and an integer min of te: C4 0.418 -> 0.415 ms, C5 6.75 -> 6.71, C3
-        // 0.254 -> 0.247; profiles/r03_ab_node_lim.txt)
-        const float lim = kAnyHit ? tx * 1.00001f : fminf(tx * 1.00001f, R.tcull);
-        tc[k] = te <= lim ? te : INFINITY;
+    for (int h = 0; h < 2; ++h) {   // children 2h, 2h + 1
+        const f2 nx = h ? f2{nd.n[0].z, nd.n[0].w} : f2{nd.n[0].x, nd.n[0].y};
+        const f2 ny = h ? f2{nd.n[1].z, nd.n[1].w} : f2{nd.n[1].x, nd.n[1].y};
+        const f2 nz = h ? f2{nd.n[2].z, nd.n[2].w} : f2{nd.n[2].x, nd.n[2].y};
+        const f2 fx = h ? f2{nd.f[0].z, nd.f[0].w} : f2{nd.f[0].x, nd.f[0].y};
+        const f2 fy = h ? f2{nd.f[1].z, nd.f[1].w} : f2{nd.f[1].x, nd.f[1].y};
+        const f2 fz = h ? f2{nd.f[2].z, nd.f[2].w} : f2{nd.f[2].x, nd.f[2].y};
+        const f2 a = pk_fma_xy(nx, R.ax), b = pk_fma_xy(ny, R.ay), c = pk_fma_xy(nz, R.az);
+        const f2 d = pk_fma_x_x(fx, R.ax, R.fxy), e = pk_fma_x_y(fy, R.ay, R.fxy), f = pk_fma_x_x(fz, R.az, R.fzc);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            // max(tnx, tny, tnz, 0) and min(tfx, tfy, tfz) as v_max3/v_min3 on the packed results
+            // (compiled fmaxf/fminf would first canonicalise each asm output: no NaN reaches here)
+            float te, tx;
+            asm("v_max3_f32 %0, %1, %2, %3\n\tv_max_f32 %0, 0, %0" : "=&v"(te) : "v"(j ? a.y : a.x), "v"(j ? b.y : b.x), "v"(j ? c.y : c.x));
+            asm("v_min3_f32 %0, %1, %2, %3" : "=v"(tx) : "v"(j ? d.y : d.x), "v"(j ? e.y : e.x), "v"(j ? f.y : f.x));
+            const float lim = kAnyHit ? tx * 1.00001f : fminf(tx * 1.00001f, tcull);
+            tc[2 * h + j] = te <= lim ? te : INFINITY;
+        }
     }
+#else
+    {
+        const float nx[4] = {nd.n[0].x, nd.n[0].y, nd.n[0].z, nd.n[0].w}, fx[4] = {nd.f[0].x, nd.f[0].y, nd.f[0].z, nd.f[0].w};
+        const float ny[4] = {nd.n[1].x, nd.n[1].y, nd.n[1].z, nd.n[1].w}, fy[4] = {nd.f[1].x, nd.f[1].y, nd.f[1].z, nd.f[1].w};
+        const float nz[4] = {nd.n[2].x, nd.n[2].y, nd.n[2].z, nd.n[2].w}, fz[4] = {nd.f[2].x, nd.f[2].y, nd.f[2].z, nd.f[2].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float tnx = fmaf(nx[k], R.ax.x, R.ax.y), tfx = fmaf(fx[k], R.ax.x, R.fxy.x);
+            const float tny = fmaf(ny[k], R.ay.x, R.ay.y), tfy = fmaf(fy[k], R.ay.x, R.fxy.y);
+            const float tnz = fmaf(nz[k], R.az.x, R.az.y), tfz = fmaf(fz[k], R.az.x, R.fzc.x);
+            const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
+            const float tx = fminf(fminf(tfx, tfy), tfz);
+            const float lim = kAnyHit ? tx * 1.00001f : fminf(tx * 1.00001f, tcull);
+            tc[k] = te <= lim ? te : INFINITY;
+        }
+    }
+#endif
     if (!kAnyHit) {
         // Sorted, branch-free pushes: the wanted children after the first go to the stack with
         // unconditional LDS writes when every lane's stack has room (slots past the new top are
@@ -487,13 +561,7 @@ __device__ __forceinline__ int32_t node4_next(const Ray4 &R, const Node4Rows &nd
             if (tc[1] != INFINITY) stack.push(sp, rc[1]);
         }
         if (nh > 0) return rc[0];
-        if (__all(sp <= stack.cap)) {
-            const int32_t top = stack.lds[max(sp - 1, 0) * stack.width + lane];
-            const int32_t r = sp > base ? top : kDoneRef;
-            sp = max(sp - 1, base);
-            return r;
-        }
-        return sp > base ? stack.pop(sp) : kDoneRef;
+        return stack.pop_or(sp, base, kDoneRef);
     }
     // any-hit: any order finds the same verdict; visit the first wanted child, push the others
     int32_t nxt = kDoneRef;
@@ -507,7 +575,7 @@ __device__ __forceinline__ int32_t node4_next(const Ray4 &R, const Node4Rows &nd
         }
     }
     if (have) return nxt;
-    return sp > base ? stack.pop(sp) : kDoneRef;
+    return stack.pop_or(sp, base, kDoneRef);
 }
 
 // The per-ray traversal constants of the four-wide walk (pad = the kernel's off-plane pad).
@@ -527,16 +595,24 @@ __device__ __forceinline__ void ray4_setup(const DevScene &sc, V3 o, V3 dir, Ray
     pad = 64.0f * 5.9604645e-08f * (fabsf(o.x) + fabsf(o.y) + fabsf(o.z) + sc.scene_m1);
     // 1.00001 / |dir| with v_rsq_f32 (1 ulp) rounded up by 1e-4: never below the division form
     R.inv_dlen = __builtin_amdgcn_rsqf(dot(dir, dir)) * 1.00011f;
-    R.o = o;
-    R.inv = inv;
     const bool nx = inv.x < 0, ny = inv.y < 0, nz = inv.z < 0;
     const float pnx = nx ? pad : -pad, pny = ny ? pad : -pad, pnz = nz ? pad : -pad;   // near = lo - pad / hi + pad
-    R.bnx = (pnx - o.x) * inv.x; R.bny = (pny - o.y) * inv.y; R.bnz = (pnz - o.z) * inv.z;
-    R.bfx = (-pnx - o.x) * inv.x; R.bfy = (-pny - o.y) * inv.y; R.bfz = (-pnz - o.z) * inv.z;
+    R.ax = f2{inv.x, (pnx - o.x) * inv.x};
+    R.ay = f2{inv.y, (pny - o.y) * inv.y};
+    R.az = f2{inv.z, (pnz - o.z) * inv.z};
+    R.fxy = f2{(-pnx - o.x) * inv.x, (-pny - o.y) * inv.y};
+    R.fzc = f2{(-pnz - o.z) * inv.z, INFINITY};   // tcull
     constexpr uint32_t kLo = offsetof(Bvh4F, lo), kHi = offsetof(Bvh4F, hi), kRow = sizeof(float4);
     R.rows[0] = (nx ? kHi : kLo); R.rows[1] = (ny ? kHi : kLo) + kRow; R.rows[2] = (nz ? kHi : kLo) + 2 * kRow;
     R.rows[3] = (nx ? kLo : kHi); R.rows[4] = (ny ? kLo : kHi) + kRow; R.rows[5] = (nz ? kLo : kHi) + 2 * kRow;
-    R.tcull = INFINITY;
+}
+
+#ifndef RT_POP_FAST
+#define RT_POP_FAST 1   // the walks' own pops (postponement, leaf loop) through LaneStack::pop_or
+#endif
+__device__ __forceinline__ int32_t walk_pop(const LaneStack &stack, int &sp, int base) {
+    if (RT_POP_FAST) return stack.pop_or(sp, base, kDoneRef);
+    return sp > base ? stack.pop(sp) : kDoneRef;
 }
 
 template <bool kAnyHit>
@@ -558,7 +634,7 @@ __device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, 
             node = node4_next<kAnyHit>(R, load_node4(sc.nodes4f, node, R.rows), stack, sp);
             if (node < 0 && node != kDoneRef && leaf == kDoneRef) {   // postpone it, keep walking
                 leaf = node;
-                node = sp ? stack.pop(sp) : kDoneRef;
+                node = walk_pop(stack, sp, 0);
             }
             if (__all(leaf != kDoneRef)) break;   // every lane still walking holds a leaf
         }
@@ -569,18 +645,18 @@ __device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, 
             // one triangle per iteration: the ref is the cursor (first + 1, count - 1), so a lane
             // whose leaf ends goes on to its next leaf while the others test their next triangle
             const TriRec T = leaf_rec(sc, first);
-            test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first]), o, dir, best, bidx, bI, done);
+            test_triangle<kAnyHit, true, RT_LEAF_SIGN>(T, static_cast<int>(sc.leaf_idx[first]), o, dir, best, bidx, bI, done);
             ++tests;
             if (kAnyHit && done) { node = kDoneRef; break; }
             if (cnt > 1) {
                 leaf = static_cast<int32_t>(u + 1u - (1u << kBvhCountShift));
                 continue;
             }
-            if (!kAnyHit && best < FLT_MAX) R.tcull = cull_param(R, best, pad);
+            if (!kAnyHit && best < FLT_MAX) R.fzc.y = cull_param(R, best, pad);
             leaf = kDoneRef;
             if (node < 0 && node != kDoneRef) {
                 leaf = node;
-                node = sp ? stack.pop(sp) : kDoneRef;
+                node = walk_pop(stack, sp, 0);
             }
         }
         if (node == kDoneRef) break;
@@ -655,7 +731,7 @@ __device__ __forceinline__ void bvh4_query_steal(const DevScene &sc, V3 o, V3 di
                 best = __uint_as_float(static_cast<uint32_t>(sk >> 32));
                 bidx = static_cast<int>(static_cast<uint32_t>(sk));
                 pidx = bidx;
-                if (!kAnyHit) R.tcull = cull_param(R, best, pad);
+                if (!kAnyHit) R.fzc.y = cull_param(R, best, pad);
             }
         }
         if (node == kDoneRef && leaf == kDoneRef) { owner = -1; sp = base; }   // (an abandoned any-hit walk's stack too)
@@ -695,7 +771,7 @@ __device__ __forceinline__ void bvh4_query_steal(const DevScene &sc, V3 o, V3 di
                 o = ho; dir = hd;
                 best = hb; bidx = hi; pidx = hi;   // the donor's best bounds the final minimum: cull with it
                 ray4_setup(sc, o, dir, R, pad);
-                if (!kAnyHit && best < FLT_MAX) R.tcull = cull_param(R, best, pad);
+                if (!kAnyHit && best < FLT_MAX) R.fzc.y = cull_param(R, best, pad);
                 done = false;
                 sp = 0; base = 0;
                 node = ref;
@@ -708,7 +784,7 @@ __device__ __forceinline__ void bvh4_query_steal(const DevScene &sc, V3 o, V3 di
             node = node4_next<kAnyHit>(R, load_node4(sc.nodes4f, node, R.rows), stack, sp, base);
             if (node < 0 && node != kDoneRef && leaf == kDoneRef) {   // postpone it, keep walking
                 leaf = node;
-                node = sp > base ? stack.pop(sp) : kDoneRef;
+                node = walk_pop(stack, sp, base);
             }
             if (__all(leaf != kDoneRef)) break;
         }
@@ -717,18 +793,18 @@ __device__ __forceinline__ void bvh4_query_steal(const DevScene &sc, V3 o, V3 di
             const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
             const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
             const TriRec T = leaf_rec(sc, first);
-            test_triangle<kAnyHit, true>(T, static_cast<int>(sc.leaf_idx[first]), o, dir, best, bidx, bI, done);
+            test_triangle<kAnyHit, true, RT_LEAF_SIGN>(T, static_cast<int>(sc.leaf_idx[first]), o, dir, best, bidx, bI, done);
             ++tests;
             if (kAnyHit && done) { node = kDoneRef; leaf = kDoneRef; break; }
             if (cnt > 1) {
                 leaf = static_cast<int32_t>(u + 1u - (1u << kBvhCountShift));
                 continue;
             }
-            if (!kAnyHit && best < FLT_MAX) R.tcull = cull_param(R, best, pad);
+            if (!kAnyHit && best < FLT_MAX) R.fzc.y = cull_param(R, best, pad);
             leaf = kDoneRef;
             if (node < 0 && node != kDoneRef) {
                 leaf = node;
-                node = sp > base ? stack.pop(sp) : kDoneRef;
+                node = walk_pop(stack, sp, base);
             }
         }
     }

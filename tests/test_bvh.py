@@ -225,3 +225,26 @@ def test_acceptance_claim_with_in_plane_pads_on_axis_aligned_slivers():
             ext = np.asarray(hi, np.float64) - np.asarray(lo, np.float64)
             assert ext[axis] < 1e-3 * ext[ax].max(), (ext, axis)
     assert n_box >= 80 and accepted > 3000
+
+
+def test_acceptance_claim_on_slivers_up_to_the_tree_limit():
+    """Slivers of 0.85-1.05 degree, on both sides of the tree's K eps limit (RT_BVH_MAX_KE 0.2,
+    ~1 degree): rays aimed at their edges and vertices, grazing and from far away, against the
+    oracle's arithmetic for those that get a box; those above the limit must be classified
+    'always tested'."""
+    rng = np.random.default_rng(47)
+    n_box = n_always = accepted = 0
+    for i in range(48):
+        theta = np.deg2rad(rng.uniform(0.85, 1.05))
+        L = 10 ** rng.uniform(-3, 2)
+        base = rng.normal(size=3) * 10 ** rng.uniform(-1, 2)
+        e1 = rng.normal(size=3); e1 /= np.linalg.norm(e1)
+        e2 = rng.normal(size=3); e2 -= (e2 @ e1) * e1; e2 /= np.linalg.norm(e2)
+        la, lb = L, L * rng.uniform(0.3, 1.0)
+        T = np.stack([base, base + la * e1, base + lb * (np.cos(theta) * e1 + np.sin(theta) * e2)]).astype(np.float32)
+        for far in (False, True):
+            st, n = _check_triangle(T, _rays_near(T, rng, 8000, far=far))
+            n_box += st == 0
+            n_always += st == 1
+            accepted += n
+    assert n_box >= 10 and n_always >= 10 and accepted > 1000

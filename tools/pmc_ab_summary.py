@@ -16,7 +16,8 @@ for d in sorted(glob.glob(os.path.join(root, "lib_*"))):
         continue
     rows = [r for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
             for r in csv.DictReader(open(f))]
-    prod = [r for r in rows if "k_chain<4, true, false, true>" in r["Kernel_Name"]]
+    # the production chain kernel: k_chain<4, true, false, true[, steal]> with the plain walk
+    prod = [r for r in rows if "k_chain<4, true, false, true" in r["Kernel_Name"] and "true, false, true, true" not in r["Kernel_Name"]]
     disp = sorted({int(r["Dispatch_Id"]) for r in prod})[1:]   # drop the first launch
     acc = collections.defaultdict(float)
     for r in prod:
@@ -24,7 +25,7 @@ for d in sorted(glob.glob(os.path.join(root, "lib_*"))):
             acc[r["Counter_Name"]] += float(r["Counter_Value"])
     n = max(len(disp), 1)
     tr = [r for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True) for r in csv.DictReader(open(f))
-          if "k_chain<4, true, false, true>" in r["Kernel_Name"] and int(r["Dispatch_Id"]) in disp]
+          if "k_chain<4, true, false, true" in r["Kernel_Name"] and int(r["Dispatch_Id"]) in disp]
     us = sum((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in tr) / max(len(tr), 1)
     res[os.path.basename(d)] = {"launches": len(disp), "kernel_us": round(us, 1), **{k: round(v / n) for k, v in sorted(acc.items())}}
 print(json.dumps(res, indent=1))
