@@ -482,6 +482,27 @@ __device__ __forceinline__ float cull_param(const Ray4 &R, float best, float pad
     return (best * 1.00002f + pad) * R.inv_dlen;
 }
 
+#ifndef RT_LIM_ASM
+#define RT_LIM_ASM 0   // min(tx (1 + 1e-5), tcull) as v_min_f32 in asm: compiled fminf re-canonicalises tcull each visit
+#endif
+#ifndef RT_ALWAYS_SORT
+#define RT_ALWAYS_SORT 0   // closest-hit: sort every node's keys (no nh count, no one-child branch)
+#endif
+#ifndef RT_TX_SLACK
+#define RT_TX_SLACK 1   // the 1e-5 relative slack of te <= tx (0: A/B measurement only)
+#endif
+template <bool kAnyHit>
+__device__ __forceinline__ float node_lim(float tx, float tcull) {
+    const float txs = RT_TX_SLACK ? tx * 1.00001f : tx;
+    if (kAnyHit) return txs;
+    if (RT_LIM_ASM) {
+        float lim;
+        asm("v_min_f32 %0, %1, %2" : "=v"(lim) : "v"(txs), "v"(tcull));
+        return lim;
+    }
+    return fminf(txs, tcull);
+}
+
 // One node visit: the wanted children by entry distance, the far ones pushed; returns the next ref
 // (the nearest wanted child, else the stack top, else kDoneRef). Entries [base, sp) are this walk's.
 template <bool kAnyHit>
@@ -514,8 +535,7 @@ __device__ __forceinline__ int32_t node4_next(const Ray4 &R, const Node4Rows &nd
             float te, tx;
             asm("v_max3_f32 %0, %1, %2, %3\n\tv_max_f32 %0, 0, %0" : "=&v"(te) : "v"(j ? a.y : a.x), "v"(j ? b.y : b.x), "v"(j ? c.y : c.x));
             asm("v_min3_f32 %0, %1, %2, %3" : "=v"(tx) : "v"(j ? d.y : d.x), "v"(j ? e.y : e.x), "v"(j ? f.y : f.x));
-            const float lim = kAnyHit ? tx * 1.00001f : fminf(tx * 1.00001f, tcull);
-            tc[2 * h + j] = te <= lim ? te : INFINITY;
+            tc[2 * h + j] = te <= node_lim<kAnyHit>(tx, tcull) ? te : INFINITY;
         }
     }
 #else
@@ -530,8 +550,7 @@ __device__ __forceinline__ int32_t node4_next(const Ray4 &R, const Node4Rows &nd
             const float tnz = fmaf(nz[k], R.az.x, R.az.y), tfz = fmaf(fz[k], R.az.x, R.fzc.x);
             const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
             const float tx = fminf(fminf(tfx, tfy), tfz);
-            const float lim = kAnyHit ? tx * 1.00001f : fminf(tx * 1.00001f, tcull);
-            tc[k] = te <= lim ? te : INFINITY;
+            tc[k] = te <= node_lim<kAnyHit>(tx, tcull) ? te : INFINITY;
         }
     }
 #endif
@@ -539,6 +558,28 @@ __device__ __forceinline__ int32_t node4_next(const Ray4 &R, const Node4Rows &nd
         // Sorted, branch-free pushes: the wanted children after the first go to the stack with
         // unconditional LDS writes when every lane's stack has room (slots past the new top are
         // scratch); pops the same way. Misses are INFINITY and sort last.
+        const int lane = static_cast<int>(threadIdx.x);
+        if (RT_ALWAYS_SORT) {
+            cswap(tc[0], rc[0], tc[1], rc[1]);
+            cswap(tc[2], rc[2], tc[3], rc[3]);
+            cswap(tc[0], rc[0], tc[2], rc[2]);
+            cswap(tc[1], rc[1], tc[3], rc[3]);
+            cswap(tc[1], rc[1], tc[2], rc[2]);
+            // the wanted children are a prefix of the sorted keys
+            const bool w1 = tc[1] != INFINITY, w2 = tc[2] != INFINITY, w3 = tc[3] != INFINITY;
+            if (__all(sp + 3 <= stack.cap)) {
+                stack.lds[sp * stack.width + lane] = w3 ? rc[3] : w2 ? rc[2] : rc[1];
+                stack.lds[(sp + 1) * stack.width + lane] = w3 ? rc[2] : rc[1];
+                stack.lds[(sp + 2) * stack.width + lane] = rc[1];
+                sp += static_cast<int>(w1) + static_cast<int>(w2) + static_cast<int>(w3);
+            } else {
+                if (w3) stack.push(sp, rc[3]);
+                if (w2) stack.push(sp, rc[2]);
+                if (w1) stack.push(sp, rc[1]);
+            }
+            if (tc[0] != INFINITY) return rc[0];
+            return stack.pop_or(sp, base, kDoneRef);
+        }
         const int nh = (tc[0] != INFINITY) + (tc[1] != INFINITY) + (tc[2] != INFINITY) + (tc[3] != INFINITY);
         if (nh > 1) {   // (the 5-exchange network costs ~25 VALU; nodes with one child or none skip it)
             cswap(tc[0], rc[0], tc[1], rc[1]);
@@ -549,7 +590,6 @@ __device__ __forceinline__ int32_t node4_next(const Ray4 &R, const Node4Rows &nd
         } else {
             rc[0] = tc[0] != INFINITY ? rc[0] : tc[1] != INFINITY ? rc[1] : tc[2] != INFINITY ? rc[2] : rc[3];
         }
-        const int lane = static_cast<int>(threadIdx.x);
         if (__all(sp + 3 <= stack.cap)) {
             stack.lds[sp * stack.width + lane] = nh == 4 ? rc[3] : nh == 3 ? rc[2] : rc[1];
             stack.lds[(sp + 1) * stack.width + lane] = nh == 4 ? rc[2] : rc[1];
