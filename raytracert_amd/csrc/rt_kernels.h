@@ -163,7 +163,7 @@ void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t strea
 constexpr int kOrderBuckets = 128;
 constexpr uint32_t kCostSplit = 0x80000000u;   // batch_cost flag: the batch ran split (lifetime in bits 0-30)
 constexpr int kWaveBatch = 64;   // lanes per wave batch of the chain launch (one sample per lane)
-constexpr int kChainMaxLights = 32;   // the chain launch's per-step shadow mask; more lights: per-step kernels
+constexpr int kChainMaxLights = RT_MAX_LIGHTS;   // the chain launch reads its lights from its arguments; more: per-step kernels
 hipError_t launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream);
 // A cold launch's batch scores (no measured order yet): one primary walk per wave batch of a fused
 // launch (g, fuse_spp, capacity as launch_chain's), scored into score[batch] for launch_order_batches.

@@ -50,13 +50,16 @@ __device__ __forceinline__ V3 ld3(const float4 &v) { return mk(v.x, v.y, v.z); }
 
 // Light l (MyLightPositions[l], raytracing.h:9): the first RT_MAX_LIGHTS ride in the kernel arguments,
 // the rest (an unbounded list, as the reference's std::vector) come from the device copy light_ext.
+// kExt false: the chain launch, which runs only with <= RT_MAX_LIGHTS lights (kChainMaxLights), reads
+// the kernel arguments alone (r04: the per-lane l < RT_MAX_LIGHTS select cost C5 1.7%, C4 0.8%).
+template <bool kExt = true>
 __device__ __forceinline__ V3 light_at(const float (&inl)[RT_MAX_LIGHTS][3], const float *ext, int l) {
-    if (l < RT_MAX_LIGHTS) return mk(inl[l][0], inl[l][1], inl[l][2]);
+    if (!kExt || l < RT_MAX_LIGHTS) return mk(inl[l][0], inl[l][1], inl[l][2]);
     return mk(ext[3 * l], ext[3 * l + 1], ext[3 * l + 2]);
 }
-// (The chain launch carries one chain step's shadow verdicts as a 32-bit mask, so it serves up to 32
-// lights, kChainMaxLights; with more, up to RT_LIGHTS_LIMIT, the render runs the per-step kernels,
-// whose verdicts are bytes per (query, light) in the workspace: rt_capi.cpp run_chain.)
+// (The chain launch serves up to kChainMaxLights = RT_MAX_LIGHTS lights, the ones in its arguments;
+// with more, up to RT_LIGHTS_LIMIT, the render runs the per-step kernels, whose verdicts are bytes
+// per (query, light) in the workspace: rt_capi.cpp run_chain.)
 
 // acosf(check) in (0, 2] for check < 0 (raytracing.cpp:296-298): glibc's acosf crosses 2.0
 // exactly once on [-1, 0), at -0x1.aa226cp-2 (acosf of it is 2.0f); verified exhaustively by
@@ -1417,7 +1420,7 @@ __device__ __forceinline__ void offset_point(V3 &point, V3 dest) {   // addOffse
 // record (local colour and child state, the child's coefficient, the depth when the chain ends)
 // and returns the secondary ray, if any. ray = dest - origin of the traced ray (:393);
 // is_shadowed(l) is isShadow's verdict for light l.
-template <bool kInLane = false, typename Shadowed>
+template <bool kInLane = false, bool kExtLights = true, typename Shadowed>
 __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadeParams &p, const DevWork &w, int step,
                                                int sample, V3 ray, int lvl, int idx, V3 P,
                                                Shadowed &&is_shadowed) {
@@ -1438,7 +1441,7 @@ __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadePa
     V3 color = mk(0, 0, 0);                                          // :336
     if ((f & RT_AMBIENT) && (m.flags & RT_HAS_KA)) color = add(color, Ka);   // :337-340
     for (int l = 0; l < p.n_lights; ++l) {                           // :342
-        const V3 L = light_at(p.lights, p.light_ext, l);
+        const V3 L = light_at<kExtLights>(p.lights, p.light_ext, l);
         const bool shadowed = (f & RT_SHADOWS) ? is_shadowed(l) : false;
         if (shadowed) continue;
         if ((f & RT_DIFFUSE) && (m.flags & RT_HAS_KD)) {             // diffuseOnly :197-205
@@ -1680,7 +1683,7 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
         for (int l = role; l < p.n_lights; l += roles) {
             int sidx = -1;
             V3 sI = mk(0, 0, 0);
-            const V3 Lp = light_at(p.lights, p.light_ext, l);
+            const V3 Lp = light_at<false>(p.lights, p.light_ext, l);   // (the chain launch: <= RT_MAX_LIGHTS)
             const V3 sd = mk(Lp.x - so.x, Lp.y - so.y, Lp.z - so.z);
             bvh_query_w<kAnyHit, W, kSteal>(sc, so, sd, true, sidx, sI, stack, ws.tests, ws.visits);
             if (sidx >= 0 && !sc.mats[sc.tri_mat[sidx]].transparent) mask |= 1u << l;   // :253-257
@@ -1696,7 +1699,7 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
         lvl = as_int(park.get(3));
         sample = as_int(park.get(4));
     }
-    return shade_hit<kInLane>(sc, p, w, step, sample, ray, lvl, bidx, bI, [&](int l) { return ((mask >> l) & 1u) != 0; });
+    return shade_hit<kInLane, false>(sc, p, w, step, sample, ray, lvl, bidx, bI, [&](int l) { return ((mask >> l) & 1u) != 0; });
 }
 
 // The chain launch: steps first..max_lvl of every query, each lane carrying its own ray through

@@ -3,8 +3,8 @@
 * Any number of lights (VERDICT r03 "What's missing" 1): the reference's MyLightPositions is an
   unbounded std::vector (raytracing.h:9) that 'L' grows (main.cpp:334-336) and shade() loops over
   in order (raytracing.cpp:342-356). rt_params.light_list carries more than RT_MAX_LIGHTS (16);
-  17-32 lights run in the chain launch (its shadow mask is 32 bits), 33 and more in the per-step
-  kernels. Whole frames with 17, 32, 33 and 64 lights equal the oracle's, on the opaque and the
+  up to 16 run in the chain launch (from its arguments), 17 and more in the per-step kernels (r04;
+  r03-r04 ran 17-32 in the chain launch). Whole frames with 17, 32, 33 and 64 lights equal the oracle's, on the opaque and the
   transparent sphere grids and on dodgeColorTest; rt_trace_rays and the debug trace too.
 * rt_trace_frame_samples: every sub-sample of the 'r' loop (main.cpp:369-388) in the loop's call
   order, with the ray the device made for it. The rays equal the loop's binary32 expressions
@@ -121,7 +121,7 @@ def test_trace_frame_samples_match_loop_and_oracle(spec, w, h, pf, max_lvl, nl, 
     """Records of rt_trace_frame_samples: rays = the loop's (bitwise); per-pixel ordered sums / spp,
     clamped = the oracle frame (bitwise); sampled colours = the oracle's trace of the same ray; the
     colour-only layout = the colours of the ray layout; ray counts = the frame's. pf 9 (81 sub-samples
-    per pixel) takes the unfused path, 20 lights the chain launch with the device light list."""
+    per pixel) takes the unfused path, 20 lights the per-step kernels with the device light list."""
     path = scene_path(spec, workdir)
     lights = _lights(nl) if nl > 2 else [(0.0, 0.0, 4.0), (1.5, 1.5, 4.0)][:nl]
     p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=max_lvl, lights=lights)
