@@ -233,6 +233,17 @@ int  rt_comm_check(rt_comm *comm);
  * polls the communicator). */
 int rt_render_frames_sharded(rt_scene *scene, const rt_params *params, rt_comm *comm, int32_t tile_w, int32_t tile_h,
                              int32_t frames, void *d_frames_out, size_t out_capacity, void *stream, uint64_t counts[3]);
+/* Pipelining of rt_render_frames_sharded (collective: every rank sets the same depth; synchronises
+ * the device). depth 1 (default): render, gather and un-permute in order on the caller's stream.
+ * depth 2: call i renders on the communicator's render stream i % 2 into one of two alternating
+ * shard buffers and gathers + un-permutes on its exchange stream; the caller's stream waits for
+ * that call's un-permute (d_frames_out is ready in stream order, as at depth 1), but the next call's
+ * render does not wait for the caller's stream, so it overlaps this call's gather and un-permute,
+ * and this call's render too when the scene keeps frames in flight (RT_TUNE_FRAMES_IN_FLIGHT 2).
+ * The gather and un-permute still follow the caller's work queued before the call.
+ * The host must then keep d_frames_out of consecutive calls distinct until its stream has passed
+ * them. Calls with counts != NULL drain the pipeline and run as at depth 1. */
+int rt_comm_set_pipeline(rt_comm *comm, int32_t depth);
 /* The un-permute step alone: d_gathered = nranks shards of slots = ceil(frames*T / nranks) tiles
  * each (tile g in shard g % nranks, slot g / nranks; tile_w*tile_h*3 bytes per tile, row-major
  * inside the tile) -> d_frames_out as above. For hosts that gather with their own transport. */

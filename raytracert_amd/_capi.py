@@ -136,6 +136,7 @@ _SIGNATURES = {
     "rt_comm_destroy": ([_VP], None),
     "rt_comm_info": ([_VP, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)], C.c_int),
     "rt_comm_check": ([_VP], C.c_int),
+    "rt_comm_set_pipeline": ([_VP, C.c_int32], C.c_int),
     "rt_render_frames_sharded": ([_VP, C.POINTER(RtParams), _VP, C.c_int32, C.c_int32, C.c_int32, _VP, C.c_size_t, _VP,
                                   _VP], C.c_int),
     "rt_assemble_tiles_device": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP,

@@ -414,6 +414,11 @@ class Comm:
     def check(self) -> None:
         check(lib().rt_comm_check(self._h))
 
+    def set_pipeline(self, depth: int) -> None:
+        """rt_comm_set_pipeline: 2 overlaps each call's render with the previous call's gather and
+        un-permute (collective; every rank sets the same depth)."""
+        check(lib().rt_comm_set_pipeline(self._h, depth))
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             lib().rt_comm_destroy(self._h)

@@ -74,6 +74,15 @@ struct rt_comm {
     ncclComm_t nccl = nullptr;
     uint8_t *shard = nullptr, *gathered = nullptr;   // device: this rank's tiles; rank 0: all ranks' tiles
     size_t shard_bytes = 0;
+    // Pipelined calls (rt_comm_set_pipeline 2): call i renders on rstream[i % 2] into shard i % 2,
+    // the gather and the un-permute run on xstream in call order; the caller's stream waits only for
+    // its own call's un-permute, so call i+1's render runs while call i's gather and un-permute do
+    // (and beside call i's render too when the scene keeps frames in flight, RT_TUNE_FRAMES_IN_FLIGHT).
+    int depth = 1, next = 0;
+    hipStream_t rstream[2] = {}, xstream = nullptr;
+    uint8_t *shard2 = nullptr;
+    hipEvent_t rendered[2] = {}, gathered_ev[2] = {}, done = nullptr, entered = nullptr;
+    bool pending[2] = {false, false};
 };
 
 using namespace rt;
@@ -118,8 +127,39 @@ void rt_comm_destroy(rt_comm *c) {
     hipDeviceSynchronize();
     if (c->nccl) rccl().comm_destroy(c->nccl);
     hipFree(c->shard);
+    hipFree(c->shard2);
     hipFree(c->gathered);
+    for (int b = 0; b < 2; ++b) {
+        if (c->rendered[b]) hipEventDestroy(c->rendered[b]);
+        if (c->gathered_ev[b]) hipEventDestroy(c->gathered_ev[b]);
+    }
+    if (c->done) hipEventDestroy(c->done);
+    if (c->entered) hipEventDestroy(c->entered);
+    for (int b = 0; b < 2; ++b)
+        if (c->rstream[b]) hipStreamDestroy(c->rstream[b]);
+    if (c->xstream) hipStreamDestroy(c->xstream);
     delete c;
+}
+
+int rt_comm_set_pipeline(rt_comm *c, int32_t depth) {
+    if (!c) return set_error(RT_E_ARG, "comm is NULL");
+    if (depth != 1 && depth != 2) return set_error(RT_E_ARG, "pipeline depth must be 1 or 2");
+    RT_HIP(hipSetDevice(c->device));
+    RT_HIP(hipDeviceSynchronize());   // (no call of the old depth is still in flight)
+    if (depth == 2 && !c->xstream) {   // streams and events made here, never inside the frame loop
+        for (int b = 0; b < 2; ++b) RT_HIP(hipStreamCreateWithFlags(&c->rstream[b], hipStreamNonBlocking));
+        RT_HIP(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
+        for (int b = 0; b < 2; ++b) {
+            RT_HIP(hipEventCreateWithFlags(&c->rendered[b], hipEventDisableTiming));
+            RT_HIP(hipEventCreateWithFlags(&c->gathered_ev[b], hipEventDisableTiming));
+        }
+        RT_HIP(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
+        RT_HIP(hipEventCreateWithFlags(&c->entered, hipEventDisableTiming));
+    }
+    c->depth = depth;
+    c->next = 0;
+    c->pending[0] = c->pending[1] = false;
+    return RT_OK;
 }
 
 int rt_comm_info(const rt_comm *c, int32_t *rank, int32_t *nranks, int32_t *device) {
@@ -174,13 +214,54 @@ int rt_render_frames_sharded(rt_scene *scene, const rt_params *params, rt_comm *
     if (shard > c->shard_bytes) {   // equal-sized shards (padded): one gather of fixed counts
         RT_HIP(hipDeviceSynchronize());
         hipFree(c->shard);
+        hipFree(c->shard2);
         hipFree(c->gathered);
-        c->shard = c->gathered = nullptr;
+        c->shard = c->shard2 = c->gathered = nullptr;
         c->shard_bytes = 0;
         RT_HIP(hipMalloc(&c->shard, shard));
+        RT_HIP(hipMalloc(&c->shard2, shard));
         if (c->rank == 0) RT_HIP(hipMalloc(&c->gathered, shard * static_cast<size_t>(c->nranks)));
         RT_HIP(hipMemset(c->shard, 0, shard));
+        RT_HIP(hipMemset(c->shard2, 0, shard));
         c->shard_bytes = shard;
+        c->pending[0] = c->pending[1] = false;
+    }
+    if (c->depth == 2 && !counts) {
+        // render on rstream[b] into shard b once the gather that last read it is done, then
+        // gather + un-permute on xstream; the caller's stream waits for this call's un-permute only.
+        // The render reads no caller-stream data (the scene and its device arrays are the library's,
+        // the parameters travel as kernel arguments), so it does not wait for the caller's stream.
+        const int b = c->next;
+        c->next ^= 1;
+        uint8_t *buf = b ? c->shard2 : c->shard;
+        hipStream_t rs = c->rstream[b];
+        if (c->pending[b]) RT_HIP(hipStreamWaitEvent(rs, c->gathered_ev[b], 0));
+        int32_t n = 0;
+        int rc = rt_render_tiles_device(scene, params, tile_w, tile_h, frames, c->rank, c->nranks, buf, c->shard_bytes,
+                                        rs, &n, nullptr);
+        if (rc) return rc;
+        RT_HIP(hipEventRecord(c->rendered[b], rs));
+        RT_HIP(hipStreamWaitEvent(c->xstream, c->rendered[b], 0));
+        // the caller's earlier work (e.g. on d_frames_out) comes before this call's un-permute writes
+        RT_HIP(hipEventRecord(c->entered, st));
+        RT_HIP(hipStreamWaitEvent(c->xstream, c->entered, 0));
+        const ncclResult_t e = rccl().gather(buf, c->gathered, shard, ncclUint8, 0, c->nccl, c->xstream);
+        if (e != ncclSuccess) return rccl_fail("ncclGather", e);
+        RT_HIP(hipEventRecord(c->gathered_ev[b], c->xstream));
+        c->pending[b] = true;
+        if (c->rank == 0) {
+            rc = rt_assemble_tiles_device(c->device, params->width, params->height, tile_w, tile_h, frames, c->nranks,
+                                          c->gathered, shard * static_cast<size_t>(c->nranks), d_frames_out, out_capacity,
+                                          c->xstream);
+            if (rc) return rc;
+        }
+        RT_HIP(hipEventRecord(c->done, c->xstream));
+        RT_HIP(hipStreamWaitEvent(st, c->done, 0));
+        return RT_OK;
+    }
+    if (c->depth == 2) {   // a call with counts synchronises anyway: drain the pipeline first
+        for (int b = 0; b < 2; ++b) RT_HIP(hipStreamSynchronize(c->rstream[b]));
+        RT_HIP(hipStreamSynchronize(c->xstream));
     }
     int32_t n = 0;
     int rc = rt_render_tiles_device(scene, params, tile_w, tile_h, frames, c->rank, c->nranks, c->shard, c->shard_bytes,

@@ -76,6 +76,54 @@ def test_render_frames_sharded_world1(workdir, gpu_available):
     comm.close()
 
 
+def test_render_frames_sharded_pipelined_world1(workdir, gpu_available):
+    """rt_comm_set_pipeline 2: each call renders on the communicator's render
+    stream into one of two alternating shards while the previous call gathers and un-permutes on the
+    exchange stream (and, with the scene's frames in flight, beside the previous call's render).
+    Twelve back-to-back calls (one and two frames each) into three rotating output
+    buffers, with no host synchronisation between them: every output equals the one-GPU frame once
+    the caller's stream has passed it; a counted call in the middle drains the pipeline; depth 1
+    again afterwards."""
+    import torch
+    comm = R.Comm(0, 0, 1, R.Comm.unique_id())
+    p = R.RenderParams(width=320, height=180, pf=2, max_lvl=3, lights=LIGHTS)
+    st = torch.cuda.current_stream()
+    with R.Scene.load(scene_path("syn:C4", workdir), device=0) as sc:
+        full, c1 = _frame(sc, p)
+        comm.set_pipeline(2)
+        for frames, fif in ((1, 1), (2, 1), (1, 2), (2, 2)):
+            sc.tune("frames_in_flight", fif)   # (2: consecutive calls' renders overlap too)
+            outs = [torch.full((frames * 180 * 320 * 3,), 7, dtype=torch.uint8, device="cuda:0") for _ in range(3)]
+            for i in range(12):
+                o = outs[i % 3]
+                if i >= 3:   # written by call i - 3: check it before reusing it
+                    st.synchronize()
+                    got = o.view(frames, 180, 320, 3).cpu().numpy()
+                    for f in range(frames):
+                        assert np.array_equal(got[f], full), (frames, fif, i - 3, f)
+                    o.fill_(7)
+                if i == 6:   # a counted call drains the pipeline and runs in order
+                    c = sc.render_frames_sharded(p, comm, 16, 16, frames, o.data_ptr(), o.numel(), st.cuda_stream,
+                                                 want_counts=True)
+                    assert [int(x) for x in c] == [frames * int(x) for x in c1]
+                else:
+                    sc.render_frames_sharded(p, comm, 16, 16, frames, o.data_ptr(), o.numel(), st.cuda_stream)
+            st.synchronize()
+            for o in outs:
+                got = o.view(frames, 180, 320, 3).cpu().numpy()
+                for f in range(frames):
+                    assert np.array_equal(got[f], full), (frames, fif)
+        sc.tune("frames_in_flight", 1)
+        comm.set_pipeline(1)
+        out = torch.zeros(180 * 320 * 3, dtype=torch.uint8, device="cuda:0")
+        sc.render_frames_sharded(p, comm, 16, 16, 1, out.data_ptr(), out.numel(), st.cuda_stream)
+        assert np.array_equal(out.view(180, 320, 3).cpu().numpy(), full)
+        with pytest.raises(R.RtError):
+            comm.set_pipeline(3)
+    comm.check()
+    comm.close()
+
+
 WORKER = r"""
 import sys, numpy as np, torch
 sys.path[:0] = [sys.argv[5], sys.argv[5] + "/tests"]
