@@ -705,7 +705,9 @@ inline void yourDebugDraw() {
 // yourKeyboardFunc (raytracing.cpp:453-553): '1'-'6' toggle Ambient, Diffuse, Specular, Reflection,
 // Shadows, Refraction; '+'/'-' step both pixel factors (clamped at 1); '0' toggles the ray debugger;
 // 'd' (debugger on) shoots the ray through the mouse position (produceRay), records (origin, first
-// hit) and prints the ray's colour, through rt_debug_trace (the per-bounce records of trace());
+// hit) and, as trace() does in DebugMode, (origin, hit) of every trace() call of the chain that hit,
+// and prints the ray's colour, through rt_debug_trace (the per-bounce records of trace()). (trace()'s
+// DebugMode records of 'r' frames, every ray of the frame, are not kept: they only feed the debug draw.)
 // 'c' clears the recorded rays; 'w' toggles wire frame. Then the settings, as the reference prints them.
 inline void yourKeyboardFunc(char key, int x, int y) {
     using rtamd_dropin::DebugMode;
@@ -735,14 +737,27 @@ inline void yourKeyboardFunc(char key, int x, int y) {
                 Vec3Df origin, dest;
                 produceRay(x, y, origin, dest);
                 const rt_params p = rtamd_dropin::params(max_lvl);
-                rt_debug_bounce b[1];
+                // every trace() call of the chain, in call order (at most two per level: reflection, refraction)
+                std::vector<rt_debug_bounce> b(static_cast<size_t>(max_lvl > 0 ? max_lvl : 0) * 2 + 2);
                 int32_t nb = 0;
                 Vec3Df color;
-                rtamd_dropin::check(rt_debug_trace(rtamd_dropin::need_scene(), &p, origin.p, dest.p, b, 1, &nb, color.p));
-                // intersectMesh's point (raytracing.cpp:498-502): the first bounce's hit, (0,0,0) on a miss
+                rtamd_dropin::check(rt_debug_trace(rtamd_dropin::need_scene(), &p, origin.p, dest.p, b.data(),
+                                                   static_cast<int32_t>(b.size()), &nb, color.p));
+                if (static_cast<size_t>(nb) > b.size()) {   // (a deeper chain than the estimate: fetch it whole)
+                    b.resize(static_cast<size_t>(nb));
+                    rtamd_dropin::check(rt_debug_trace(rtamd_dropin::need_scene(), &p, origin.p, dest.p, b.data(), nb, &nb,
+                                                       color.p));
+                }
+                // intersectMesh's point (raytracing.cpp:498-502): the first bounce's hit, (0,0,0) on a miss;
+                // then, as trace() does in DebugMode (:398-401), (origin, hit) of every call that hit
                 rtamd_dropin::debug_origins.push_back(origin);
                 rtamd_dropin::debug_hits.push_back(nb > 0 && b[0].triangle >= 0 ? Vec3Df(b[0].hit[0], b[0].hit[1], b[0].hit[2])
                                                                                : Vec3Df(0, 0, 0));
+                for (int32_t i = 0; i < nb; ++i) {
+                    if (b[i].triangle < 0) continue;
+                    rtamd_dropin::debug_origins.push_back(Vec3Df(b[i].origin[0], b[i].origin[1], b[i].origin[2]));
+                    rtamd_dropin::debug_hits.push_back(Vec3Df(b[i].hit[0], b[i].hit[1], b[i].hit[2]));
+                }
                 char buffer[128];
                 std::cout << "Ray trace color = " << color.toString(buffer, sizeof(buffer)) << std::endl;
             }

@@ -259,7 +259,13 @@ int main(int argc, char **argv) {
             produceRay(x, y, o, d);
             std::printf("dray %08x %08x %08x %08x %08x %08x\n", bits(o[0]), bits(o[1]), bits(o[2]), bits(d[0]), bits(d[1]),
                         bits(d[2]));
+            const size_t before = rtamd_dropin::debug_origins.size();
             keyboard('d', x, y);
+            for (size_t j = before; j < rtamd_dropin::debug_origins.size(); ++j) {   // what 'd' recorded
+                const Vec3Df &a = rtamd_dropin::debug_origins[j], &h = rtamd_dropin::debug_hits[j];
+                std::printf("dpair %08x %08x %08x %08x %08x %08x\n", bits(a[0]), bits(a[1]), bits(a[2]), bits(h[0]), bits(h[1]),
+                            bits(h[2]));
+            }
         } else if (k[0] == 'R') {
             render_one_call();
         } else if (k[0] == 'T') {

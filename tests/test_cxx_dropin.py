@@ -132,11 +132,25 @@ def test_dropin_key_session_matches_oracle(spec, w, h, dropin_bin, workdir, tmp_
     cols = [l for l in lines if l.startswith("Ray trace color = ")]
     assert len(drays) == len(cols) == 2
     p = O.make_params(w, h, pf=2, max_lvl=10, lights=[(0.0, 0.0, 4.0)] * 2, flags=_flags("111000"))   # shadows off then
-    for r, c in zip(drays, cols):
+    # the recorded (origin, hit) pairs of each 'd' (raytracing.cpp:498-502, then trace()'s :398-401 per call that hit)
+    groups, cur = [], None
+    for l in lines:
+        if l.startswith("dray "):
+            cur = []
+            groups.append(cur)
+        elif l.startswith("dpair "):
+            cur.append(np.array([int(x, 16) for x in l.split()[1:]], np.uint32))
+    assert len(groups) == 2
+    for r, c, pairs in zip(drays, cols, groups):
         v = np.array([int(x, 16) for x in r], np.uint32).view(np.float32)
-        _, rgb = orc.debug_trace(p, v[:3], v[3:])
+        recs, rgb = orc.debug_trace(p, v[:3], v[3:])
         got = np.array([float(x) for x in c.split("(")[1].rstrip(")").split(",")], np.float32)
         assert np.abs(got - rgb).max() <= 1e-6 + F32_TOL
+        first = recs[0]["hit"] if recs and recs[0]["triangle"] >= 0 else np.zeros(3, np.float32)
+        want = [np.concatenate([v[:3], first])] + [np.concatenate([b["origin"], b["hit"]]) for b in recs if b["triangle"] >= 0]
+        assert len(pairs) == len(want)
+        for a, b in zip(pairs, want):
+            assert np.array_equal(a, np.asarray(b, np.float32).view(np.uint32))
     assert "Ray trace history cleared" in lines
 
 
