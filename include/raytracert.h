@@ -126,7 +126,23 @@ int  rt_scene_load_obj(const char *path, int32_t device, rt_scene **out);
 #define RT_LOAD_PARALLEL   0
 #define RT_LOAD_SEQUENTIAL 1
 #define RT_LOAD_THREADS(n) ((n) << 8)   /* with RT_LOAD_PARALLEL: exactly n parser threads (tests) */
+/* | RT_LOAD_TEXCOORDS: also keep Mesh::texcoords and Triangle::t (mesh.cpp:199-209, 263-268,
+ * 290-316; the sequential parse), read back with rt_scene_texcoords. The tracer never uses them. */
+#define RT_LOAD_TEXCOORDS  0x10
 int  rt_scene_load_obj_ex(const char *path, int32_t device, int32_t load_flags, rt_scene **out);
+/* Texture coordinates of a scene loaded with RT_LOAD_TEXCOORDS: *n_texcoords `vt` entries as 3
+ * floats each (x, y, 0: the reference reads 2D coordinates into a Vec3Df), and per triangle its
+ * three texture-coordinate indices (Triangle::t: the face's 1-based indices minus 1, as unsigned;
+ * 0 for corners without one, mesh.cpp:290-291). Any pointer may be NULL; sizes 3*n, 3*nt. */
+int  rt_scene_texcoords(const rt_scene *scene, int32_t *n_texcoords, float *texcoords, uint32_t *tri_t);
+/* Mesh::loadMtl's parse (mesh.cpp:334-460) of one MTL file: every block the reference would
+ * commit, in file order (unset values inherited from the previous block, `d` and `Tr` both set
+ * Tr). Mesh::loadMtl then appends each block whose name is not yet in its materialIndex (the
+ * first of a name wins). *n_blocks = the count; materials (capacity entries, may be NULL) and
+ * names (NUL-separated, may be NULL; names_capacity must hold them all) receive them.
+ * RT_E_IO if the file cannot be opened (the reference prints a warning and returns false). */
+int  rt_load_mtl(const char *path, int32_t *n_blocks, rt_material *materials, int32_t capacity, char *names,
+                 size_t names_capacity);
 int  rt_scene_create(const float *xyz, int32_t n_vertices, const uint32_t *tri_v, const uint32_t *tri_mat,
                      int32_t n_triangles, const rt_material *materials, int32_t n_materials,
                      int32_t device, rt_scene **out);

@@ -42,10 +42,12 @@
  * Extra: RayTracerDevice (the GPU init() binds; RT_HOST_ONLY = loader only), uploadMesh() (re-upload
  * MyMesh after editing it), renderImage() (the 'r' loop in one call, Image::_image's floats),
  * performRayTracing over vectors (batched). Failures throw rtamd_dropin::Error (the reference has no
- * error path). Not provided (never called by main.cpp, no effect on the image): Mesh::loadMtl as a
- * separate call (loadMesh loads the mtllib), the dead box/rectangle intersectors and getTeller
- * (declared, never defined by the reference). Texture coordinates are not loaded (Mesh::texcoords
- * stays empty, Triangle::t = 0): the render path never reads them. Header-only; C++17; -lrtamd.
+ * error path). Mesh::texcoords and Triangle::t are loaded as mesh.cpp loads them
+ * (RT_LOAD_TEXCOORDS) and Mesh::loadMtl is a separate call too (rt_load_mtl), though the render
+ * path reads neither. Not provided (never called by main.cpp, no effect on the image): the dead
+ * box/rectangle intersectors and getTeller (declared, never defined by the reference), and
+ * trace()'s DebugMode records of 'r' frames (every ray of a frame; they only feed the debug draw).
+ * Header-only; C++17; -lrtamd.
  */
 #ifndef RAYTRACERT_DROPIN_HPP_
 #define RAYTRACERT_DROPIN_HPP_
@@ -193,8 +195,16 @@ class Triangle {
         v[0] = v0; v[1] = v1; v[2] = v2;
         t[0] = t0; t[1] = t1; t[2] = t2;
     }
+    Triangle(const Triangle &o) = default;
+    // mesh.h:150-158 as written: assignment copies the vertex indices into t too (the copy
+    // constructor, which loadMesh's push_back uses, copies t)
+    Triangle &operator=(const Triangle &o) {
+        v[0] = o.v[0]; v[1] = o.v[1]; v[2] = o.v[2];
+        t[0] = o.v[0]; t[1] = o.v[1]; t[2] = o.v[2];
+        return *this;
+    }
     unsigned int v[3];   // vertex indices
-    unsigned int t[3];   // texture-coordinate indices (not loaded here: 0)
+    unsigned int t[3];   // texture-coordinate indices (Mesh::texcoords)
 };
 
 class Material {
@@ -277,7 +287,7 @@ class Mesh {
     // crashes there, mesh.cpp:329)
     bool loadMesh(const char *filename, bool /*randomizeTriangulation: disabled in the reference too*/) {
         rt_scene *s = nullptr;
-        if (rt_scene_load_obj(filename, RT_HOST_ONLY, &s) != RT_OK) return false;
+        if (rt_scene_load_obj_ex(filename, RT_HOST_ONLY, RT_LOAD_SEQUENTIAL | RT_LOAD_TEXCOORDS, &s) != RT_OK) return false;
         int32_t nv = 0, nt = 0, nm = 0;
         rt_scene_info(s, &nv, &nt, &nm);
         std::vector<float> xyz(3 * static_cast<size_t>(nv));
@@ -285,15 +295,49 @@ class Mesh {
         std::vector<rt_material> mats(static_cast<size_t>(nm));
         triangleMaterials.assign(static_cast<size_t>(nt), 0u);
         rt_scene_export(s, xyz.data(), tv.data(), triangleMaterials.data(), mats.data(), nullptr);
+        int32_t ntc = 0;
+        rt_scene_texcoords(s, &ntc, nullptr, nullptr);
+        std::vector<float> tc(3 * static_cast<size_t>(ntc));
+        std::vector<uint32_t> tt(3 * static_cast<size_t>(nt));
+        rt_scene_texcoords(s, &ntc, tc.data(), tt.data());
         rt_scene_destroy(s);
         vertices.assign(static_cast<size_t>(nv), Vertex());
         for (int32_t i = 0; i < nv; ++i) vertices[i].p = Vec3Df(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]);
         triangles.assign(static_cast<size_t>(nt), Triangle());
         for (int32_t i = 0; i < nt; ++i)
-            for (int k = 0; k < 3; ++k) triangles[i].v[k] = tv[3 * i + k];
+            for (int k = 0; k < 3; ++k) {
+                triangles[i].v[k] = tv[3 * i + k];
+                triangles[i].t[k] = tt[3 * i + k];
+            }
         materials.clear();
         for (const rt_material &m : mats) materials.push_back(Material::from_rt(m));
-        texcoords.clear();
+        texcoords.assign(static_cast<size_t>(ntc), Vec3Df());
+        for (int32_t i = 0; i < ntc; ++i) texcoords[i] = Vec3Df(tc[3 * i], tc[3 * i + 1], tc[3 * i + 2]);
+        return true;
+    }
+    // Mesh::loadMtl (mesh.cpp:334-460): appends each block of the file whose name materialIndex does
+    // not hold yet and indexes it; false (with the reference's warning) if the file cannot be read
+    bool loadMtl(const char *filename, std::map<std::string, unsigned int> &materialIndex) {
+        int32_t n = 0;
+        if (rt_load_mtl(filename, &n, nullptr, 0, nullptr, 0) != RT_OK) {
+            std::printf("  Warning! Material file '%s' not found!\n", filename);
+            return false;
+        }
+        std::vector<rt_material> mats(static_cast<size_t>(n));
+        size_t cap = 1;
+        for (int32_t i = 0; i < n; ++i) cap += 256;   // (a name is at most one 256-byte line)
+        std::vector<char> names(cap);
+        if (rt_load_mtl(filename, &n, mats.data(), n, names.data(), names.size()) != RT_OK) return false;
+        const char *nm = names.data();
+        for (int32_t i = 0; i < n; ++i) {
+            const std::string key(nm);
+            nm += key.size() + 1;
+            if (materialIndex.find(key) != materialIndex.end()) continue;
+            Material m = Material::from_rt(mats[static_cast<size_t>(i)]);
+            m.set_name(key);
+            materials.push_back(m);
+            materialIndex[key] = static_cast<unsigned int>(materials.size() - 1);
+        }
         return true;
     }
     // Mesh::computeVertexNormals (mesh.cpp:28-47): the sum of the adjacent face normals, normalised

@@ -54,6 +54,7 @@ BVH_INFO_FIELDS = 7
 STOCHASTIC = 1 << 8
 DEFAULT_SEED = 0x5EED
 LOAD_PARALLEL, LOAD_SEQUENTIAL = 0, 1
+LOAD_TEXCOORDS = 0x10
 WORK_FIELDS = 6
 
 
@@ -131,6 +132,8 @@ _SIGNATURES = {
     "rt_scene_bvh_validate": ([_VP], C.c_int),
     "rt_bvh_acceptance_box": ([_VP, _VP, _VP], C.c_int),
     "rt_scene_tune": ([_VP, C.c_int32, C.c_int32], C.c_int),
+    "rt_scene_texcoords": ([_VP, C.POINTER(C.c_int32), _VP, _VP], C.c_int),
+    "rt_load_mtl": ([C.c_char_p, C.POINTER(C.c_int32), _VP, C.c_int32, C.c_char_p, C.c_size_t], C.c_int),
     "rt_comm_unique_id": ([_VP], C.c_int),
     "rt_comm_init": ([C.c_int32, C.c_int32, C.c_int32, _VP, C.POINTER(_VP)], C.c_int),
     "rt_comm_destroy": ([_VP], None),

@@ -88,12 +88,15 @@ class Scene:
 
     # -- construction ------------------------------------------------------------------------
     @classmethod
-    def load(cls, path: str, device: int = 0, sequential: bool = False, threads: int = 0) -> "Scene":
+    def load(cls, path: str, device: int = 0, sequential: bool = False, threads: int = 0,
+             texcoords: bool = False) -> "Scene":
         """init(fileName): Mesh::loadMesh + loadMtl + calculateNormals. The default parser is
         parallel (threads=0: automatic); sequential=True runs the line-by-line restatement (same
-        result)."""
+        result); texcoords=True also keeps Mesh::texcoords / Triangle::t (Scene.texcoords())."""
         h = C.c_void_p()
         flags = _capi.LOAD_SEQUENTIAL if sequential else (_capi.LOAD_PARALLEL | (int(threads) << 8))
+        if texcoords:
+            flags |= _capi.LOAD_TEXCOORDS
         check(lib().rt_scene_load_obj_ex(path.encode(), device, flags, C.byref(h)))
         return cls(h, device)
 
@@ -153,6 +156,16 @@ class Scene:
         mat_list = [dict(Kd=tuple(m.Kd), Ka=tuple(m.Ka), Ks=tuple(m.Ks), Ns=m.Ns, Ni=m.Ni, Tr=m.Tr,
                          illum=m.illum, flags=m.flags) for m in list(mats)[:nm]]
         return dict(vertices=verts, triangles=tri, tri_mat=tmat, materials=mat_list, normals=normals)
+
+    def texcoords(self) -> tuple[np.ndarray, np.ndarray]:
+        """rt_scene_texcoords (a scene loaded with texcoords=True): (texcoords[n, 3] float32 with z = 0,
+        tri_t[nt, 3] uint32), Mesh::texcoords and each Triangle::t."""
+        n = C.c_int32()
+        check(lib().rt_scene_texcoords(self._h, C.byref(n), None, None))
+        tc = np.zeros((n.value, 3), np.float32)
+        tt = np.zeros((self.counts()[1], 3), np.uint32)
+        check(lib().rt_scene_texcoords(self._h, C.byref(n), _ptr(tc), _ptr(tt)))
+        return tc, tt
 
     def get_material(self, triangle_index: int) -> dict:
         m = RtMaterial()
@@ -370,6 +383,22 @@ class Scene:
         out["simd_eff_visits"] = out["visits"] / max(1, 64 * out["wave_max_visits"])
         out["simd_eff_tests"] = out["tests"] / max(1, 64 * out["wave_max_tests"])
         return out
+
+
+def load_mtl(path: str) -> list[tuple[str, dict]]:
+    """rt_load_mtl: every block Mesh::loadMtl would commit from one MTL file, in file order, as
+    (name, material); the caller keeps the first block of each name not already indexed."""
+    n = C.c_int32()
+    check(lib().rt_load_mtl(path.encode(), C.byref(n), None, 0, None, 0))
+    mats = (RtMaterial * max(n.value, 1))()
+    cap = 1
+    with open(path, "rb") as f:   # (names are at most the file's bytes)
+        cap += len(f.read()) + n.value
+    names = C.create_string_buffer(cap)
+    check(lib().rt_load_mtl(path.encode(), C.byref(n), C.cast(mats, C.c_void_p), n.value, names, cap))
+    raw = names.raw.split(b"\0")[: n.value]
+    return [(nm.decode(), dict(Kd=tuple(m.Kd), Ka=tuple(m.Ka), Ks=tuple(m.Ks), Ns=m.Ns, Ni=m.Ni, Tr=m.Tr,
+                               illum=m.illum, flags=m.flags)) for nm, m in zip(raw, list(mats)[: n.value])]
 
 
 def bvh_acceptance_box(T) -> tuple[int, np.ndarray, np.ndarray]:

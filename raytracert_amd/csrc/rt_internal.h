@@ -25,11 +25,20 @@ struct HostScene {
     std::vector<uint32_t> tri_mat;   // per triangle
     std::vector<HostMaterial> mats;  // index 0 = default material (mesh.cpp:108-117)
     std::vector<float> normals;      // 3 per triangle (calculateNormals, raytracing.cpp:78-86)
+    // Mesh::texcoords and Triangle::t (mesh.cpp:199-209, 263-268, 290-316), kept only when the scene
+    // is loaded with RT_LOAD_TEXCOORDS (the tracer never reads them)
+    bool has_texcoords = false;
+    std::vector<float> texcoords;    // 3 per `vt` line (x, y, 0)
+    std::vector<uint32_t> tri_t;     // 3 per triangle
 };
 
 // OBJ/MTL loader with Mesh::loadMesh / loadMtl semantics (mesh.cpp:95-460).
 // Returns RT_OK or RT_E_IO; warnings go to stderr like the reference's printf.
-int load_obj(const char *path, HostScene &out, std::string &err);
+int load_obj(const char *path, HostScene &out, std::string &err, bool texcoords = false);
+// Mesh::loadMtl's parse (mesh.cpp:334-460) without the name filter: every block the reference
+// would commit (name and material, in file order, unset values inherited from the previous block);
+// loadMtl keeps the first block of each name not already indexed. false if the file cannot be opened.
+bool parse_mtl(const std::string &filename, std::vector<HostMaterial> &blocks);
 // calculateNormals (raytracing.cpp:78-86), binary32 without contraction.
 void compute_face_normals(HostScene &s);
 

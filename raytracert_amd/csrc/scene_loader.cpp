@@ -42,25 +42,19 @@ constexpr int kLineLen = 256;   // mesh.cpp:22
 constexpr uint32_t kValidMask = RT_HAS_KD | RT_HAS_KA | RT_HAS_KS | RT_HAS_TR;  // is_valid(), mesh.h:55-56
 
 
-// Mesh::loadMtl, mesh.cpp:334-460
-void load_mtl(const std::string &filename, HostScene &s, MtlIndex &index) {
+// Mesh::loadMtl, mesh.cpp:334-460: every block it would commit, in order (the name filter is the caller's)
+bool parse_mtl_file(const std::string &filename, std::vector<HostMaterial> &blocks) {
     FILE *in = std::fopen(filename.c_str(), "r");
-    if (!in) {
-        std::fprintf(stderr, "  Warning! Material file '%s' not found!\n", filename.c_str());
-        return;
-    }
+    if (!in) return false;
     char line[kLineLen];
     std::string key;
     HostMaterial mat;            // zeroed: never-set values read 0
     float f1 = 0, f2 = 0, f3 = 0;
     bool indef = false;
     auto commit = [&]() {
-        if (index.find(key) < 0) {
-            HostMaterial m = mat;
-            m.name = key;
-            s.mats.push_back(m);
-            index.by_name[key] = static_cast<int>(s.mats.size()) - 1;
-        }
+        HostMaterial m = mat;
+        m.name = key;
+        blocks.push_back(m);
     };
     std::memset(line, 0, kLineLen);
     while (!std::feof(in)) {
@@ -106,9 +100,26 @@ void load_mtl(const std::string &filename, HostScene &s, MtlIndex &index) {
         std::memset(line, 0, kLineLen);
     }
     std::fclose(in);
+    return true;
+}
+
+// Mesh::loadMtl into the scene: the blocks whose name is not yet indexed (materialIndex.find(key) == end)
+void load_mtl(const std::string &filename, HostScene &s, MtlIndex &index) {
+    std::vector<HostMaterial> blocks;
+    if (!parse_mtl_file(filename, blocks)) {
+        std::fprintf(stderr, "  Warning! Material file '%s' not found!\n", filename.c_str());
+        return;
+    }
+    for (const HostMaterial &m : blocks) {
+        if (index.find(m.name) >= 0) continue;
+        s.mats.push_back(m);
+        index.by_name[m.name] = static_cast<int>(s.mats.size()) - 1;
+    }
 }
 
 }  // namespace
+
+bool parse_mtl(const std::string &filename, std::vector<HostMaterial> &blocks) { return parse_mtl_file(filename, blocks); }
 
 // The OBJ reader's material state (mesh.cpp:108-117 default material, :157-178 mtllib, :180-193
 // usemtl), shared by the sequential and the parallel parser so both replay it identically.
@@ -164,16 +175,20 @@ void finish_obj(HostScene &s) {
         if (s.tris[3 * i] < nv && s.tris[3 * i + 1] < nv && s.tris[3 * i + 2] < nv) {
             s.tris[3 * k] = s.tris[3 * i]; s.tris[3 * k + 1] = s.tris[3 * i + 1]; s.tris[3 * k + 2] = s.tris[3 * i + 2];
             s.tri_mat[k] = s.tri_mat[i];
+            if (s.has_texcoords)
+                for (int j = 0; j < 3; ++j) s.tri_t[3 * k + j] = s.tri_t[3 * i + j];
             ++k;
         }
     }
     s.tris.resize(3 * k);
     s.tri_mat.resize(k);
+    if (s.has_texcoords) s.tri_t.resize(3 * k);
     compute_face_normals(s);
 }
 
-int load_obj(const char *path, HostScene &s, std::string &err) {
+int load_obj(const char *path, HostScene &s, std::string &err, bool texcoords) {
     s = HostScene();
+    s.has_texcoords = texcoords;
     FILE *in = std::fopen(path, "r");
     if (!in) {
         err = std::string("cannot open OBJ file '") + path + "'";
@@ -182,8 +197,9 @@ int load_obj(const char *path, HostScene &s, std::string &err) {
     ObjControlState cs(path, s);
     char line[kLineLen];
     float x = 0, y = 0, z = 0;
-    std::vector<int> vh;
+    std::vector<int> vh, th;   // vhandles, texhandles (mesh.cpp:218-288)
     vh.reserve(64);
+    th.reserve(64);
     std::memset(line, 0, kLineLen);
     while (!std::feof(in) && std::fgets(line, kLineLen, in)) {
         const char c0 = line[0];
@@ -194,11 +210,16 @@ int load_obj(const char *path, HostScene &s, std::string &err) {
         if (c0 == 'v' && line[1] == ' ') {
             std::sscanf(line, "v %f %f %f", &x, &y, &z);
             s.verts.push_back(x); s.verts.push_back(y); s.verts.push_back(z);
+        } else if (texcoords && std::strncmp(line, "vt ", 3) == 0) {   // mesh.cpp:199-209: 2D, z = 0
+            float t[3] = {0, 0, 0};
+            std::sscanf(line, "vt %f %f", &t[0], &t[1]);
+            s.texcoords.push_back(t[0]); s.texcoords.push_back(t[1]); s.texcoords.push_back(t[2]);
         } else if (c0 == 'f' && line[1] == ' ') {
             int component = 0;
             bool endOfVertex = false;
             char *p0, *p1 = line + 2;
             vh.clear();
+            th.clear();
             while (*p1 == ' ') ++p1;
             while (p1) {
                 p0 = p1;
@@ -207,21 +228,31 @@ int load_obj(const char *path, HostScene &s, std::string &err) {
                 if (*p1 != '\0') { *p1 = '\0'; ++p1; }
                 if (*p1 == '\0' || *p1 == '\n') p1 = nullptr;
                 if (*p0 != '\0' && component == 0) vh.push_back(std::atoi(p0) - 1);
+                if (*p0 != '\0' && component == 1 && texcoords) th.push_back(std::atoi(p0) - 1);
                 ++component;
                 if (endOfVertex) { component = 0; endOfVertex = false; }
             }
             const int m = cs.current_material();
             bool bad = false;
             for (int v : vh) bad |= (v < 0);
+            if (texcoords && th.size() != vh.size()) th.resize(vh.size(), 0);   // mesh.cpp:290-291
             if (!bad) {
                 if (vh.size() > 3) {
                     for (size_t i = 0; i + 2 < vh.size(); ++i) {
                         s.tris.push_back(uint32_t(vh[0])); s.tris.push_back(uint32_t(vh[i + 1]));
                         s.tris.push_back(uint32_t(vh[i + 2])); s.tri_mat.push_back(uint32_t(m));
+                        if (texcoords) {
+                            s.tri_t.push_back(uint32_t(th[0])); s.tri_t.push_back(uint32_t(th[i + 1]));
+                            s.tri_t.push_back(uint32_t(th[i + 2]));
+                        }
                     }
                 } else if (vh.size() == 3) {
                     s.tris.push_back(uint32_t(vh[0])); s.tris.push_back(uint32_t(vh[1]));
                     s.tris.push_back(uint32_t(vh[2])); s.tri_mat.push_back(uint32_t(m));
+                    if (texcoords) {
+                        s.tri_t.push_back(uint32_t(th[0])); s.tri_t.push_back(uint32_t(th[1]));
+                        s.tri_t.push_back(uint32_t(th[2]));
+                    }
                 }
             }
         } else if (std::strncmp(line, "mtllib ", 7) == 0) {
@@ -229,7 +260,7 @@ int load_obj(const char *path, HostScene &s, std::string &err) {
         } else if (std::strncmp(line, "usemtl ", 7) == 0) {
             cs.usemtl(line);
         }
-        // `vt`, `vn`, `o`, `g`, `s`: not used by the tracer
+        // `vn`, `o`, `g`, `s` (and `vt` without RT_LOAD_TEXCOORDS): not used by the tracer
         std::memset(line, 0, kLineLen);
     }
     std::fclose(in);

@@ -242,6 +242,25 @@ int main(int argc, char **argv) {
         Vec3Df b(1, 2, 3);
         swap(a, b);
         std::printf("vec %g %g %s\n", Vec3Df::dotProduct(b, u), Vec3Df::dotProduct(b, v), a.toString(buf, sizeof buf));
+        // Mesh::texcoords and Triangle::t (mesh.cpp:199-209, 263-316)
+        unsigned long long htc = 1469598103934665603ull, htt = htc;
+        for (const Vec3Df &t : MyMesh.texcoords)
+            for (int k = 0; k < 3; ++k) htc = (htc ^ bits(t[k])) * 1099511628211ull;
+        for (const Triangle &t : MyMesh.triangles)
+            for (int k = 0; k < 3; ++k) htt = (htt ^ t.t[k]) * 1099511628211ull;
+        std::printf("texcoords %zu %016llx %016llx\n", MyMesh.texcoords.size(), htc, htt);
+        // Mesh::loadMtl as a separate call (argv[3]): into an empty mesh with an empty index
+        if (argc > 3) {
+            Mesh m;
+            std::map<std::string, unsigned int> index;
+            const bool ok = m.loadMtl(argv[3], index);
+            std::printf("loadmtl %d %zu", ok ? 1 : 0, m.materials.size());
+            for (const auto &kv : index) std::printf(" %s=%u", kv.first.c_str(), kv.second);
+            std::printf("\n");
+            for (const Material &mm : m.materials)
+                std::printf("mtl %s %08x %08x %08x %08x %d\n", mm.name().c_str(), bits(mm.Kd()[0]), bits(mm.Ka()[1]),
+                            bits(mm.Tr()), bits(mm.Ns()), mm.has_Ks());
+        }
         dessiner();
         return 0;
     }

@@ -188,3 +188,26 @@ def test_dropin_session_with_more_lights_than_inline(dropin_bin, workdir, tmp_pa
         ou8 = orc.render(O.make_params(40, 24, pf=1, max_lvl=10, lights=[(0.0, 0.0, 4.0)] * nl), nthreads=16)[1]
         d = np.abs(read_ppm(f[1]).astype(np.int16) - ou8.astype(np.int16))
         assert d.max() <= 1 and (d == 0).mean() >= 0.9999, f
+
+
+def test_dropin_mesh_texcoords_and_loadmtl(dropin_bin, workdir, tmp_path):
+    """Mesh::texcoords / Triangle::t as mesh.cpp loads them (cube.obj has `vt` and v/vt/vn faces),
+    equal to rt_scene_texcoords; Mesh::loadMtl as a separate call: a repeated name keeps its first
+    block, inherited values, the index the reference builds (VERDICT r03 "What's missing" 4)."""
+    path = scene_path("ref:cube.obj", workdir)
+    (tmp_path / "dup.mtl").write_text("newmtl a\nKd 1 0 0\nNs 10\n\nnewmtl b\nKa 0 1 0\n\nnewmtl a\nKd 0 0 1\n\n"
+                                      "newmtl c\nNi 1.5\n\nnewmtl d\nd 0.25\n")
+    lines = _lines([dropin_bin, "host", path, str(tmp_path / "dup.mtl")])
+    tcl = next(l.split()[1:] for l in lines if l.startswith("texcoords "))
+    import raytracert_amd as R
+    tc, tt = R.Scene.load(path, device=R.RT_HOST_ONLY, texcoords=True).texcoords()
+    assert int(tcl[0]) == len(tc) == 4
+    assert tcl[1] == _fnv(tc.reshape(-1).view(np.uint32)) and tcl[2] == _fnv(tt.reshape(-1))
+    lm = next(l.split()[1:] for l in lines if l.startswith("loadmtl "))
+    assert lm == ["1", "3", "a=0", "b=1", "d=2"]
+    mt = [l.split()[1:] for l in lines if l.startswith("mtl ")]
+    assert [m[0] for m in mt] == ["a", "b", "d"]
+    assert mt[0][1] == _bits(1.0) and mt[1][1] == _bits(1.0) and mt[1][2] == _bits(1.0)   # b inherits a's Kd
+    assert mt[2][3] == _bits(0.25) and mt[0][4] == _bits(10.0)
+    lines = _lines([dropin_bin, "host", path, str(tmp_path / "missing.mtl")])
+    assert next(l for l in lines if l.startswith("loadmtl ")).split()[1:3] == ["0", "0"]
