@@ -663,3 +663,78 @@ def test_debug_trace_matches_oracle(spec, workdir, gpu_available):
             chains += len(gb) > 1
     if spec.startswith("syn:"):   # the reference models cover a few percent of the default view
         assert chains > 5
+
+
+def _sliver_field(path, rng, n=3000):
+    """Slivers of 0.8-3 degrees at T0 (the largest acceptance pads the tree uses, and the always-tested
+    ones below ~1 degree), a third in exact axis planes, a third tilted by 1e-6..1e-2 rad, a third in
+    random orientation, packed into a box so their padded boxes overlap."""
+    lines, tris = [], []
+    for i in range(n):
+        kind = i % 3
+        theta = np.deg2rad(rng.uniform(0.8, 3.0))
+        L = 10 ** rng.uniform(-2, -0.5)
+        base = rng.uniform(-1, 1, 3)
+        if kind == 2:
+            e1 = rng.normal(size=3); e1 /= np.linalg.norm(e1)
+            e2 = rng.normal(size=3); e2 -= (e2 @ e1) * e1; e2 /= np.linalg.norm(e2)
+        else:
+            ax = i % 3 if kind == 0 else rng.integers(0, 3)
+            others = [k for k in range(3) if k != ax]
+            phi = rng.uniform(0, 2 * np.pi)
+            e1 = np.zeros(3); e2 = np.zeros(3)
+            e1[others[0]], e1[others[1]] = np.cos(phi), np.sin(phi)
+            e2[others[0]], e2[others[1]] = -np.sin(phi), np.cos(phi)
+            if kind == 1:
+                e2[ax] = np.sin(10 ** rng.uniform(-6, -2)); e2 /= np.linalg.norm(e2)
+        T = np.stack([base, base + L * e1, base + L * rng.uniform(0.3, 1) * (np.cos(theta) * e1 + np.sin(theta) * e2)])
+        tris.append(T.astype(np.float32))
+    with open(path, "w") as f:
+        for T in tris:
+            for v in T:
+                f.write("v %.9g %.9g %.9g\n" % tuple(v))
+        for i in range(n):
+            f.write("f %d %d %d\n" % (3 * i + 1, 3 * i + 2, 3 * i + 3))
+    return np.array(tris)
+
+
+@pytest.mark.parametrize("width", [2, 4])
+def test_bvh_matches_brute_force_on_sliver_field(width, workdir, gpu_available):
+    """The in-plane acceptance pads (r04) where they matter: 3,000 near-threshold slivers, axis-aligned,
+    slightly tilted and free, and 120k rays aimed within 1e-4 (barycentric) of their edges and
+    vertices from near and far, a third of them grazing. BVH (two- and four-wide) equals brute
+    force bit for bit."""
+    import os
+    rng = np.random.default_rng(41)
+    path = os.path.join(workdir, "slivers.obj")
+    tris = _sliver_field(path, rng)
+    n = 120000
+    k = rng.integers(0, len(tris), n)
+    T = tris[k].astype(np.float64)
+    u, v = T[:, 1] - T[:, 0], T[:, 2] - T[:, 0]
+    s = rng.random(n)
+    t = rng.random(n) * (1 - s)
+    kind = rng.integers(0, 4, n)
+    s = np.where(kind == 0, rng.normal(0, 1e-4, n), s)
+    t = np.where(kind == 1, rng.normal(0, 1e-4, n), t)
+    t = np.where(kind == 2, 1 - s + rng.normal(0, 1e-4, n), t)
+    P = T[:, 0] + s[:, None] * u + t[:, None] * v
+    d = rng.normal(size=(n, 3)); d /= np.linalg.norm(d, axis=1)[:, None]
+    nrm = np.cross(u, v); nrm /= np.linalg.norm(nrm, axis=1)[:, None]
+    graze = rng.random(n) < 0.33
+    d[graze] -= ((d[graze] * nrm[graze]).sum(1) * (1 - 1e-4 * rng.random(graze.sum())))[:, None] * nrm[graze]
+    d /= np.linalg.norm(d, axis=1)[:, None]
+    dist = 10 ** rng.uniform(-2, 1, n)
+    o = (P - d * dist[:, None]).astype(np.float32)
+    dst = (o + d * 10 ** rng.uniform(0, 1.5, n)[:, None]).astype(np.float32)
+    with R.Scene.load(path, device=0) as sc:
+        info = sc.bvh_info()
+        assert info["always"] > 0 and info["leaf_triangles"] > 2000
+        sc.set_accel("brute_force")
+        bi, bp = sc.intersect_mesh(o, dst)
+        sc.set_accel("bvh")
+        sc.tune("bvh_width", width)
+        vi, vp = sc.intersect_mesh(o, dst)
+    assert np.array_equal(bi, vi), np.nonzero(bi != vi)[0][:10]
+    assert np.array_equal(bp.view(np.uint32), vp.view(np.uint32))
+    assert (bi >= 0).sum() > 30000
