@@ -105,6 +105,10 @@ extern "C" {
                                     frame's blocks then fill the slots the previous frame's tail frees; block
                                     dispatch runs two frames side by side from their first blocks: C4 0.387
                                     -> 0.377 ms per frame); 0: always the trials' distribution. Placement only */
+#define RT_TUNE_INFLIGHT_STREAMS 34 /* 1: with RT_TUNE_FRAMES_IN_FLIGHT > 1, a single-pipeline call runs on its
+                                    pipeline's own stream (forked from the caller's stream and joined back),
+                                    so two frames in flight overlap whichever hardware queues the caller's
+                                    streams share; 0 (default): on the caller's stream. Placement only */
 #define RT_TUNE_TOP_NODES 13     /* retired in r03 (0-85 accepted, no effect): an LDS copy of the four-wide
                                     tree's top levels; with float node rows loaded from global memory it
                                     measured slower (flat loads, 64-bit addresses) */

@@ -50,6 +50,7 @@ TUNE_SHADOW_HELPERS = 30
 TUNE_FRAMES_IN_FLIGHT = 31
 TUNE_ADOPT_ORDER = 32
 TUNE_INFLIGHT_DYNAMIC = 33
+TUNE_INFLIGHT_STREAMS = 34
 BVH_INFO_FIELDS = 7
 STOCHASTIC = 1 << 8
 DEFAULT_SEED = 0x5EED

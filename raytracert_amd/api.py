@@ -312,7 +312,8 @@ class Scene:
              "prio_batches": _capi.TUNE_PRIORITY_BATCHES,
              "pixel_order": _capi.TUNE_PIXEL_ORDER, "dyn_group": _capi.TUNE_DYN_GROUP,
              "shadow_helpers": _capi.TUNE_SHADOW_HELPERS, "frames_in_flight": _capi.TUNE_FRAMES_IN_FLIGHT,
-             "adopt_order": _capi.TUNE_ADOPT_ORDER, "inflight_dynamic": _capi.TUNE_INFLIGHT_DYNAMIC}[knob]
+             "adopt_order": _capi.TUNE_ADOPT_ORDER, "inflight_dynamic": _capi.TUNE_INFLIGHT_DYNAMIC,
+             "inflight_streams": _capi.TUNE_INFLIGHT_STREAMS}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
 
     def trials(self) -> dict:

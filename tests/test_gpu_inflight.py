@@ -28,9 +28,10 @@ WORKLOADS = {
 }
 
 
-@pytest.mark.parametrize("fif", [2, 3])
+@pytest.mark.parametrize("fif,own", [(2, 0), (3, 0), (2, 1)])
 @pytest.mark.parametrize("name", ["c4", "ref_default"])
-def test_frames_in_flight_every_buffer_equals_one_in_flight_frame(name, fif, workdir, gpu_available):
+def test_frames_in_flight_every_buffer_equals_one_in_flight_frame(name, fif, own, workdir, gpu_available):
+    """own 1: RT_TUNE_INFLIGHT_STREAMS, each frame forked onto its pipeline's own stream."""
     import torch
     wl = WORKLOADS[name]
     w, h = wl["w"], wl["h"]
@@ -60,6 +61,7 @@ def test_frames_in_flight_every_buffer_equals_one_in_flight_frame(name, fif, wor
                 break
         assert sc.trials()["choice"] >= 0   # (the other pipelines adopt this decision and pipeline 0's order)
         sc.tune("frames_in_flight", fif)
+        sc.tune("inflight_streams", own)
         streams = [main] + [torch.cuda.Stream(dev) for _ in range(fif - 1)]
         bufs = [torch.full((h * w * 3,), 7, dtype=torch.uint8, device=dev) for _ in range(2 * fif)]
         nframes = 40
