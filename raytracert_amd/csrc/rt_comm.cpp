@@ -274,6 +274,9 @@ int rt_render_frames_sharded(rt_scene *scene, const rt_params *params, rt_comm *
                                       shard * static_cast<size_t>(c->nranks), d_frames_out, out_capacity, stream);
         if (rc) return rc;
     }
+    // (depth 2: the next call renders into a shard and gathers into `gathered` from its own streams,
+    // which do not wait for the caller's: this call's gather and un-permute finish first)
+    if (c->depth == 2) RT_HIP(hipStreamSynchronize(st));
     return counts ? rt_comm_check(c) : RT_OK;
 }
 
