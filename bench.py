@@ -210,6 +210,13 @@ def main():
                               for _ in range(max(2, args.inflight))]
                 # frames in flight: frame i on stream i % F (the first is the bench's stream)
                 self.fstreams = [stream] + [torch.cuda.Stream(dev) for _ in range(max(args.inflight, 1) - 1)]
+                # a new stream's first command initialises it (~6 ms of host time on this image): done
+                # here, at setup, not at the warm-up's second frame, where it left the GPU idle just
+                # before the timed frames (they then ran ~5% slow for ~25 frames)
+                for fs in self.fstreams[1:]:
+                    with torch.cuda.stream(fs):
+                        torch.zeros(1, device=dev).add_(1)
+                torch.cuda.synchronize(dev)
             elif rank == 0:
                 self.frames_out = [torch.zeros(frames * HEIGHT * WIDTH * 3, dtype=torch.uint8, device=dev) for _ in range(2)]
             else:
@@ -322,22 +329,31 @@ def main():
     # a renderer serving a view pays once. Bounded; the count is reported (config.calibration_frames).
     inflight = max(1, args.inflight) if main_run.single else 1
 
-    def calibrate():
+    def calibrate(fif):
+        # frames one at a time (synchronised: a trial is decided once its launches' events have
+        # completed), alternating over the F pipelines of the timed mode: pipeline 0's launches run the
+        # trials, the others adopt its order and decision, and every pipeline's one-time setup
+        # (workspace, streams) happens here rather than just before the timed frames (an idle GPU there
+        # left the next ~25 frames ~5% slow: the clock ramps back up, profiles/r04_inflight_settle.txt)
         n = 0
         if args.accel == "bvh" and rtcomm is None:   # (each rank its own view's trials, before the barrier)
-            while n < 64 and scene.trials()["choice"] < 0:
-                main_run.render_once(0)
+            while n < 64 * fif and scene.trials()["choice"] < 0:
+                main_run.render_once(n)
                 n += 1
-                torch.cuda.synchronize(dev)   # (a trial is decided once its launches' events have completed)
+                torch.cuda.synchronize(dev)
+            for _ in range((fif - n % fif) % fif):   # (end on a whole round: timed frame i takes pipeline i mod F)
+                main_run.render_once(n)
+                n += 1
+                torch.cuda.synchronize(dev)
         return n
 
-    calib = calibrate()
-    # ---- timed region (the metric) ----
     if inflight > 1:
         # the other pipelines start from pipeline 0's batch order and adopt its trial decision
-        # (rt_capi.cpp run_chain); frame i of the run after the tune takes pipeline i mod F
+        # (rt_capi.cpp run_chain); call i after the tune takes pipeline i mod F
         scene.tune("frames_in_flight", inflight)
         main_run.fif = inflight
+    calib = calibrate(inflight)
+    # ---- timed region (the metric) ----
     elapsed, frames = main_run.run(args.steps, args.warmup * inflight)
     # the last timed frame, kept before any later leg reuses its buffer: the in-run parity check
     # (cpu_baseline) reads this copy
@@ -396,7 +412,7 @@ def main():
     cold_ms = sorted(cold)[1] * 1e3 if cold else None
     cold_screen_ms = sorted(cold_screen)[1] * 1e3 if cold_screen else None
     main_run.run(0, max(args.warmup, 3))   # re-learn the measured order before the other legs
-    calibrate()                             # (and re-decide the launch trials the cold legs forgot)
+    calibrate(1)                            # (and re-decide the launch trials the cold legs forgot)
 
     # ---- the same work through the other path: N=1 the shard path (tiles + un-permute, what
     # N>1 runs, minus the collective); N>1 strong scaling (one frame split over the ranks) ----
@@ -559,8 +575,9 @@ def main():
                                    "one-in-flight loop, both measured in this run over the same K frames "
                                    "(one_in_flight holds both)",
                 "calibration_frames": calib,
-                "calibration_what": "frames rendered one at a time before the warm-up until the view's launch "
-                                    "trials were decided (rt_scene_trials; at most 64)",
+                "calibration_what": "frames rendered one at a time before the warm-up, over the F pipelines of the "
+                                    "timed mode in turn, until pipeline 0's launch trials were decided (rt_scene_trials; "
+                                    "at most 64 per pipeline), then to the end of the round",
                 "frames_in_flight_what": "consecutive frames of the view on alternating streams, each into its own "
                                          "buffer and fully rendered (RT_TUNE_FRAMES_IN_FLIGHT): a frame's launch starts "
                                          "while the previous frame's longest batches still run; ms_per_step is then "
