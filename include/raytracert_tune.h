@@ -95,7 +95,9 @@ extern "C" {
                                     a caller that queues consecutive frames on as many alternating
                                     streams keeps that many frames in flight: a frame's launch starts as
                                     the previous frame's short batches retire, beside its longest
-                                    ones. Calls on one stream stay serialised. Placement only */
+                                    ones. Calls on one stream stay serialised. Setting it makes the
+                                    other pipelines' streams, events and workspaces (pipeline 0's size)
+                                    at once, not at their first frame. Placement only */
 #define RT_TUNE_ADOPT_ORDER 32   /* 1 (default): a pipeline meeting a batch geometry that another pipeline has
                                     already ordered starts from that pipeline's measured order (frames in
                                     flight); 0: it learns its own from a cold launch. Placement only */
