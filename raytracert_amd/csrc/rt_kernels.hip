@@ -1653,6 +1653,14 @@ constexpr int kChainSteps = 256;   // max_lvl <= 254
 #ifndef RT_LDS_PARK
 #define RT_LDS_PARK 0
 #endif
+// RT_OPAQUE_ARGS 1 (default, r04): the chain kernel reads its frame geometry, shading parameters,
+// scene and workspace per wave batch through the kernel-argument pointer instead of holding them from
+// its start: 232 SGPRs had spilled into four VGPRs' lanes and pushed 48 B per lane into scratch;
+// now 72 and 24 B. C4 0.361 -> 0.348 ms per frame, C5 6.86 -> 6.68 ms, VALU -5.7%, WRITE_SIZE
+// 116 -> 72 MB per launch (profiles/r04_ab_opaque_args.txt). 0: the arguments as the compiler places them.
+#ifndef RT_OPAQUE_ARGS
+#define RT_OPAQUE_ARGS 1
+#endif
 
 constexpr int kParkWords = 8;   // words per lane of the park area: ray xyz, lvl, sample, pixel (k_chain)
 struct Park {
@@ -1740,6 +1748,20 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
 // vb < 4 s4 is quarter vb & 3 of batch order[vb >> 2]; then vb - 4 s4 < 2 s2 is half (vb - 4 s4) & 1
 // of batch order[s4 + ((vb - 4 s4) >> 1)]; later ones batch order[vb - 3 s4 - s2]. The host only
 // splits when a part holds whole pixels (launch_chain). Placement never changes results.
+// k_chain's explicit arguments as laid out in the kernel-argument segment (in order, each at its
+// natural alignment, as the members of a struct), for RT_OPAQUE_ARGS; k_chain checks the layout
+// against its own arguments at its start (a mismatch sets the error slot and ends the launch)
+struct ChainKernargs {
+    DevScene sc;
+    ShadeParams p;
+    DevWork w;
+    int first, ordered;
+    uint8_t *out_u8;
+    float *out_f32;
+    int fuse_spp, spb, nbatch;
+    FrameGeom g;
+    int split, split8;
+};
 template <int W, bool kAnyHit, bool kCount, bool kInLane = false, bool kSteal = false>
 __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kSteal ? RT_STEAL_WPE : RT_CHAIN_WPE))) void k_chain(
     const DevScene sc, const ShadeParams p, DevWork w, int first, int ordered, uint8_t *__restrict__ out_u8,
@@ -1753,6 +1775,17 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
     const Park park{nullptr};
 #endif
     for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) { s_q[i] = 0; s_sh[i] = 0; }
+#if RT_OPAQUE_ARGS
+    {   // the argument layout ChainKernargs assumes: a mismatch is an internal error, not a result
+        typedef const __attribute__((address_space(4))) ChainKernargs *KargPtr;
+        const KargPtr ka = (KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
+        if (ka->g.width != g.width || ka->p.n_lights != p.n_lights || ka->nbatch != nbatch || ka->split8 != split8 ||
+            ka->p.max_lvl != p.max_lvl || ka->g.corners[7][2] != g.corners[7][2]) {
+            if (threadIdx.x == 0) w.counters[kErrorSlot] = 1;
+            return;
+        }
+    }
+#endif
     __syncthreads();
     const LaneStack stack = lane_stack(sc, lds_stack);
     WorkTally<kCount> wc, ws;   // closest-hit and shadow work (totals only: lanes diverge here)
@@ -1775,8 +1808,24 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
     const bool dyn = kInLane && sc.chain_split == 4;
     drive_queries((nbatch + extra) * kWave, dyn ? 4 : (sc.chain_split & 3), dyn ? &w.counters[kWaveQueueSlot] : w.wq + (2 * first) * kWqSlot,
                   [&](int j0, int vend) {
+#if RT_OPAQUE_ARGS
+        // the frame geometry, shading parameters, scene and workspace are read from the kernel
+        // arguments through a pointer the compiler cannot follow across batches, so their scalar
+        // loads stay in the batch loop instead of being hoisted to the kernel's start and held
+        // (spilled into VGPR lanes, and those VGPRs into scratch) for its whole life
+        typedef const __attribute__((address_space(4))) ChainKernargs *KargPtr;
+        KargPtr ka = (KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ka));
+        const FrameGeom &gl = *(const FrameGeom *)&ka->g;
+        const ShadeParams &pl = *(const ShadeParams *)&ka->p;
+        const DevScene &scb = *(const DevScene *)&ka->sc;
+        const DevWork &wb = *(const DevWork *)&ka->w;
+#else
         const FrameGeom &gl = g;
         const ShadeParams &pl = p;
+        const DevScene &scb = sc;
+        const DevWork &wb = w;
+#endif
         const int vb = j0 >> 6;   // this wave's virtual batch (wave-uniform for the orderable distributions)
         // split tiers of the order: 8 parts, then 4, then 2; part = which part of batch order[ob]
         int ob = vb - (ordered ? extra : 0), nparts = 1, part = 0;
@@ -1787,12 +1836,12 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
             else if (v2 < 2 * s2) { nparts = 2; ob = split8 + s4 + (v2 >> 1); part = v2 & 1; }
         }
         if (ordered) {   // the longest batches (and their parts) issue first on their SIMD
-            if (ob < sc.prio_batches) __builtin_amdgcn_s_setprio(3);
+            if (ob < scb.prio_batches) __builtin_amdgcn_s_setprio(3);
             else __builtin_amdgcn_s_setprio(0);
         }
         const int plen = ((ppb + nparts - 1) / nparts) * spp;   // whole pixels per part
         const bool wave_on = (vb << 6) < vend;
-        const int pb = (ordered && wave_on) ? w.batch_order[ob] : vb;
+        const int pb = (ordered && wave_on) ? wb.batch_order[ob] : vb;
         const int lane_off = nparts > 1 ? part * plen + lane : (j0 & (kWave - 1));
         // (unordered, the XCD-segment distributions hand out unaligned ranges: the lane's own bound)
         const bool lane_on = (ordered ? wave_on : j0 < vend) && (nparts == 1 || lane < plen) && lane_off < spb;
@@ -1802,7 +1851,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         int px = -1;   // (out_mode 2: the sample's output slot, pixel x spp + sub-sample)
         // shadow helpers (RT_TUNE_SHADOW_HELPERS): in a split wave of the fused launch the lanes past
         // the part's plen samples help their owners' shadow walks, roles = lanes per sample (<= lights)
-        const int roles = (kInLane && !kSteal && nparts > 1 && sc.shadow_helpers && (pl.flags & RT_SHADOWS))
+        const int roles = (kInLane && !kSteal && nparts > 1 && scb.shadow_helpers && (pl.flags & RT_SHADOWS))
                               ? max(1, min(kWave / plen, pl.n_lights)) : 1;
         const int role = (roles > 1 && lane >= plen && lane < roles * plen) ? lane / plen : 0;
         [&]() {
@@ -1830,7 +1879,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
             sample = j;
         } else {
             if (!own) return;
-            const float4 qo = w.q_org[first & 1][j], qd = w.q_dst[first & 1][j];
+            const float4 qo = wb.q_org[first & 1][j], qd = wb.q_dst[first & 1][j];
             lvl = as_int(qd.w);
             if (lvl < 0) return;
             sample = as_int(qo.w);
@@ -1839,7 +1888,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         }
         for (int step = first; step < kChainSteps; ++step) {
             if (step > first && role == 0) atomicAdd(&s_q[step], 1);
-            const Secondary sec = chain_step<kAnyHit, W, kCount, kInLane, kSteal>(sc, pl, w, step, sample, org, dst, lvl, stack,
+            const Secondary sec = chain_step<kAnyHit, W, kCount, kInLane, kSteal>(scb, pl, wb, step, sample, org, dst, lvl, stack,
                                                                                   s_sh, wc, ws, role, roles, plen, park);
             bool cont = sec.state == kChildTrace;
             if (roles > 1) cont = __shfl(static_cast<int>(cont), role ? lane - role * plen : lane) != 0;   // the owner's
@@ -1849,7 +1898,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
             }
             if (sec.state != kChildTrace) {
                 if (kInLane)   // the chain ends here: fold it in the lane (fold_chain's arithmetic)
-                    rgb = fold_inlane(sc, w, first, step, sample,
+                    rgb = fold_inlane(scb, wb, first, step, sample,
                                       sec.state == kChildZero ? add(sec.local, mk(0.0f, 0.0f, 0.0f)) : sec.local);
                 break;
             }
@@ -1875,9 +1924,9 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         // bit 31 set for a split batch (kCostSplit): the sort counts it double, so a batch that ran
         // faster because it was split (or helped) stays at the head of the order instead of
         // dropping out of the split tier and back in on every re-sort
-        if (lane == 0 && wave_on && w.batch_cost) {   // (null: a launch with no pipeline order, rt_trace_rays)
+        if (lane == 0 && wave_on && wb.batch_cost) {   // (null: a launch with no pipeline order, rt_trace_rays)
             const uint32_t d = static_cast<uint32_t>(min(__builtin_amdgcn_s_memrealtime() - t0, 0x7FFFFFFFull));
-            w.batch_cost[pb] = nparts > 1 ? (d | kCostSplit) : d;
+            wb.batch_cost[pb] = nparts > 1 ? (d | kCostSplit) : d;
         }
     }, dyn ? sc.dyn_group_log2 : 0);
     wc.flush(sc.work);

@@ -1,10 +1,10 @@
 #!/bin/bash
 # One PMC pass (counter set $1) per A/B library raytracert_amd/ab/lib_*.so, on the bench's chain
-# kernel: gpurun_out/pmc_ab/<lib>/... (summarise with tools/pmc_ab_summary.py).
+# kernel: gpurun_out/${PMC_OUT:-pmc_ab}/<lib>/... (summarise with tools/pmc_ab_summary.py).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 C=${1:-"SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD"}
-OUT="$GRAFT_REPO_ROOT/gpurun_out/pmc_ab"
+OUT="$GRAFT_REPO_ROOT/gpurun_out/${PMC_OUT:-pmc_ab}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 300 python3 -c "import torch" || exit 1
