@@ -1658,6 +1658,8 @@ constexpr int kChainSteps = 256;   // max_lvl <= 254
 // its start: 232 SGPRs had spilled into four VGPRs' lanes and pushed 48 B per lane into scratch;
 // now 72 and 24 B. C4 0.361 -> 0.348 ms per frame, C5 6.86 -> 6.68 ms, VALU -5.7%, WRITE_SIZE
 // 116 -> 72 MB per launch (profiles/r04_ab_opaque_args.txt). 0: the arguments as the compiler places them.
+// 2: the launch's scalar arguments (outputs, first step, split tiers) too: within the spread
+// (profiles/r04_ab_opaque_args2.txt).
 #ifndef RT_OPAQUE_ARGS
 #define RT_OPAQUE_ARGS 1
 #endif
@@ -1820,6 +1822,13 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         const ShadeParams &pl = *(const ShadeParams *)&ka->p;
         const DevScene &scb = *(const DevScene *)&ka->sc;
         const DevWork &wb = *(const DevWork *)&ka->w;
+#if RT_OPAQUE_ARGS >= 2
+        uint8_t *const out_u8 = ka->out_u8;
+        float *const out_f32 = ka->out_f32;
+        const int first = ka->first, ordered = ka->ordered, fuse_spp = kInLane ? ka->fuse_spp : 0, spb = kInLane ? ka->spb : kWave;
+        const int split8 = ka->split8, s2 = ka->split & 0xFFFF, s4 = ka->split >> 16, extra = 7 * split8 + 3 * s4 + s2;
+        const int spp = kInLane ? fuse_spp : 1, ppb = spb / spp;
+#endif
 #else
         const FrameGeom &gl = g;
         const ShadeParams &pl = p;
