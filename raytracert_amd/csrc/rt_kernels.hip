@@ -718,7 +718,8 @@ __device__ __forceinline__ void bvh4_query_ww(const DevScene &sc, V3 o, V3 dir, 
 // once a helper has published one. Only placement changes, never results.
 // ---------------------------------------------------------------------------------------------
 #ifndef RT_STEAL_WPE
-#define RT_STEAL_WPE 4   // waves per EU of the stealing chain kernel (5 spills ~100 VGPRs: measured slower)
+#define RT_STEAL_WPE 4   // waves per EU of the stealing chain kernel (5 spilled ~100 VGPRs in r03; r04, with the
+                         // arguments read per batch, 88 B per lane and still slower on C2: profiles/r04_ab_steal_wpe.txt)
 #endif
 #ifndef RT_STEAL_MIN_IDLE
 #define RT_STEAL_MIN_IDLE 8   // steal only when at least this many lanes of the wave are idle
