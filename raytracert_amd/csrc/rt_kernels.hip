@@ -1783,7 +1783,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         typedef const __attribute__((address_space(4))) ChainKernargs *KargPtr;
         const KargPtr ka = (KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
         if (ka->g.width != g.width || ka->p.n_lights != p.n_lights || ka->nbatch != nbatch || ka->split8 != split8 ||
-            ka->p.max_lvl != p.max_lvl || as_int(ka->g.corners[7][2]) != as_int(g.corners[7][2])) {   // (bits: a NaN camera)
+            ka->p.max_lvl != p.max_lvl || (ka->g.corners[7][2] != g.corners[7][2] && g.corners[7][2] == g.corners[7][2])) {
             if (threadIdx.x == 0) w.counters[kErrorSlot] = 1;
             return;
         }
