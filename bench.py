@@ -115,6 +115,9 @@ def parse():
     ap.add_argument("--inflight", type=int, default=2,
                     help="N=1 frame path: frames in flight (RT_TUNE_FRAMES_IN_FLIGHT), consecutive frames "
                          "on this many alternating streams into their own buffers")
+    ap.add_argument("--orbit-step", type=float, default=0.25,
+                    help="N=1: also time a moving view, each frame the view turned by this many degrees more "
+                         "(scenes.orbit_corners; 0 = skip): config.orbit")
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
                     help="extra launch-shape knob (Scene.tune), e.g. shadow_virtual=-1; repeatable")
     return ap.parse_args()
@@ -208,8 +211,11 @@ def main():
             if frame_path:
                 self.fbufs = [torch.zeros(HEIGHT * WIDTH * 3, dtype=torch.uint8, device=dev)
                               for _ in range(max(2, args.inflight))]
-                # frames in flight: frame i on stream i % F (the first is the bench's stream)
-                self.fstreams = [stream] + [torch.cuda.Stream(dev) for _ in range(max(args.inflight, 1) - 1)]
+                # frames in flight: frame i on stream i % F (the first is the bench's stream, the others
+                # the library's rt_stream_create: each on a hardware queue of its own, so two frames never
+                # share one of the runtime's GPU_MAX_HW_QUEUES queues and run one after the other)
+                self.own_streams = [R.stream_create(local_rank) for _ in range(max(args.inflight, 1) - 1)]
+                self.fstreams = [stream] + [torch.cuda.ExternalStream(s, device=dev) for s in self.own_streams]
                 # a new stream's first command initialises it (~6 ms of host time on this image): done
                 # here, at setup, not at the warm-up's second frame, where it left the GPU idle just
                 # before the timed frames (they then ran ~5% slow for ~25 frames)
@@ -371,14 +377,14 @@ def main():
         one_in_flight = {"ms_per_step": round(el1 / args.steps * 1e3, 3),
                          "value": round(rays_per_step * args.steps / el1 / 1e6, 4),
                          "what": "the same timed loop with one frame in flight (each launch waits for the previous frame)"}
-        # the line's value is the faster of the two serving modes measured in this run (both timed
-        # over the same K frames, both fully rendered); the other is reported beside it
-        multi = {"ms_per_step": round(elapsed / args.steps * 1e3, 3),
-                 "value": round(rays_per_step * args.steps / elapsed / 1e6, 4),
-                 "what": f"{inflight} frames in flight on alternating streams"}
-        if el1 < elapsed:
-            elapsed, value_mode = el1, "one_in_flight"
-        one_in_flight["multi_in_flight"] = multi
+        # the line's value is the configured mode's (--inflight, chosen before the run); the same K
+        # frames one at a time are reported beside it
+
+    # ---- a moving view: every frame a new view of an orbit (the trackball turned, then 'r') ----
+    orbit = None
+    if main_run.single and args.orbit_step > 0 and args.accel == "bvh":
+        orbit = orbit_leg(scene, main_run, WIDTH, HEIGHT, PF, MAX_LVL, LIGHTS, flags, args, inflight, obj, dev)
+    orbit_last = orbit.pop("_last") if orbit else None
 
     rehearsal = None
     if args.rehearse and rank == 0 and frames is not None:   # every assembled frame = the one-GPU frame
@@ -571,9 +577,8 @@ def main():
                 "frame_ms_per_gpu": round(elapsed / args.steps * 1e3, 3),
                 "frames_in_flight": inflight,
                 "value_mode": value_mode,
-                "value_mode_what": "value/ms_per_step come from the faster of the frames-in-flight loop and the "
-                                   "one-in-flight loop, both measured in this run over the same K frames "
-                                   "(one_in_flight holds both)",
+                "value_mode_what": "value/ms_per_step come from the configured mode (--inflight frames in flight); "
+                                   "one_in_flight times the same K frames one at a time in the same run",
                 "calibration_frames": calib,
                 "calibration_what": "frames rendered one at a time before the warm-up, over the F pipelines of the "
                                     "timed mode in turn, until pipeline 0's launch trials were decided (rt_scene_trials; "
@@ -583,6 +588,7 @@ def main():
                                          "while the previous frame's longest batches still run; ms_per_step is then "
                                          "the per-frame throughput time, one_in_flight the frame-after-frame time",
                 "one_in_flight": one_in_flight,
+                "orbit": orbit,
                 "first_frame_ms": round(cold_ms, 3) if cold_ms is not None else None,
                 "first_frame_what": "a new view's first frame (no measured batch order or launch trial: every order "
                                     "forgotten first), dispatched centre-out (RT_TUNE_COLD_ESTIMATE 2) as dynamic "
@@ -645,6 +651,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(obj, params, timed_last[0].cpu().numpy(), layout, args, wl)
         result["cpu_baseline"]["parity_vs_gpu"]["frame"] = timed_last_what
+        if orbit_last is not None:   # the last timed orbit view, on tiles across its sphere region
+            result["config"]["orbit"]["parity_vs_cpu"] = orbit_parity(obj, params, orbit_last, wl)
 
     if rtcomm is not None:
         rtcomm.close()
@@ -653,6 +661,56 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+def orbit_leg(scene, run, W, H, PF, MAX_LVL, LIGHTS, flags, args, inflight, obj, dev):
+    """A moving view: frame i renders view i of an orbit (scenes.orbit_corners: the default view turned
+    by i * --orbit-step degrees about the world y axis, the trackball's effect on produceRay's corner
+    rays; MyCameraPosition fixed, main.cpp:222), so no two frames share a view. Warm-up frames are new
+    views too; the batch order and launch trials carry over from view to view (their key is the frame
+    geometry). Timed with the static leg's frames in flight and one at a time, every frame fully
+    rendered; rays are counted per view afterwards (each view has its own count). The last timed
+    frame is kept for the in-run oracle check (cpu_baseline)."""
+    import torch
+
+    import raytracert_amd as R
+    from raytracert_amd import scenes
+    warm, K = max(args.warmup, 2) * inflight, args.steps
+    corners = [scenes.orbit_corners(W, H, k + 1, args.orbit_step) for k in range(warm + K)]
+    views = [R.RenderParams(width=W, height=H, pf=PF, max_lvl=MAX_LVL, lights=LIGHTS, flags=flags, corners=c).to_c()
+             for c in corners]
+
+    def loop(fif, first, n):
+        scene.tune("frames_in_flight", fif)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(n):
+            fb, st = run.fbufs[i % max(2, fif)], run.fstreams[i % fif]
+            scene.render_frame_device(views[first + i], TILE, TILE, fb.data_ptr(), fb.numel(), st.cuda_stream)
+        torch.cuda.synchronize(dev)
+        return time.perf_counter() - t0
+
+    loop(inflight, 0, warm)
+    el = loop(inflight, warm, K)
+    last = run.fbufs[(K - 1) % max(2, inflight)].clone().view(H, W, 3)
+    torch.cuda.synchronize(dev)
+    el1 = loop(1, warm, K) if inflight > 1 else el
+    rays = 0
+    for k in range(warm, warm + K):
+        fb = run.fbufs[0]
+        c = scene.render_frame_device(views[k], TILE, TILE, fb.data_ptr(), fb.numel(), run.fstreams[0].cuda_stream,
+                                      want_counts=True)
+        rays += int(sum(int(x) for x in c))
+    scene.tune("frames_in_flight", 1)
+    return {"what": f"every frame a new view: the default view turned by frame x {args.orbit_step} degrees about the "
+                    f"world y axis (the trackball, then 'r'), {warm} warm-up and {K} timed views, each fully rendered; "
+                    f"order and launch trials carried over from view to view",
+            "step_deg": args.orbit_step, "views_timed": K, "first_timed_deg": round((warm + 1) * args.orbit_step, 3),
+            "frames_in_flight": inflight,
+            "ms_per_step": round(el / K * 1e3, 3), "value": round(rays / el / 1e6, 4),
+            "one_in_flight": {"ms_per_step": round(el1 / K * 1e3, 3), "value": round(rays / el1 / 1e6, 4)},
+            "rays_per_frame_mean": round(rays / K), "unit": "Mrays/s",
+            "_last": (last, corners[warm + K - 1])}
 
 
 def strong_model(t1_ms, crit_ms, shard_ms, frame_bytes, link_gbs=(50.0, 150.0), rccl_lat_ms=0.02, sync_ms=0.02):
@@ -766,6 +824,28 @@ def host_cpu():
     except (AttributeError, OSError):
         share = os.cpu_count()
     return {"nproc": os.cpu_count(), "affinity": share, "model": model or "unknown"}
+
+
+def orbit_parity(obj, params, last, wl):
+    """The in-run parity check of the orbit leg: tiles of its last timed view against the CPU
+    restatement at that view's corner rays (the cpu_baseline leg's checker)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import oracle as O
+    frame, corners = last
+    img = frame.cpu().numpy()
+    op = O.make_params(params.width, params.height, params.pf, params.max_lvl, lights=params.lights, flags=params.flags,
+                       seed=params.seed, corners=corners)
+    sc = O.OracleScene(obj)
+    w, h = params.width, params.height
+    tiles = [((w // 2 // TILE + dx) * TILE, (h // 2 // TILE + dy) * TILE) for dx, dy in ((0, 0), (-12, -8), (12, 8), (-20, 10))]
+    exact = total = max_d = 0
+    for x0, y0 in tiles:
+        _, u8, _ = sc.render(op, x0, y0, TILE, TILE, nthreads=16)
+        d = np.abs(img[y0:y0 + TILE, x0:x0 + TILE].astype(np.int16) - u8.astype(np.int16))
+        max_d, exact, total = max(max_d, int(d.max())), exact + int((d == 0).sum()), total + d.size
+    return {"tiles": tiles, "bytes": total, "exact_frac": round(exact / max(total, 1), 6), "max_lsb": max_d,
+            "frame": "the last timed orbit view"}
 
 
 def cpu_baseline(obj, params, gpu_frame, layout, args, wl):

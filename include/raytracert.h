@@ -6,6 +6,7 @@
  *   rt_scene_load_obj     init(char*)                       raytracing.h:19, raytracing.cpp:42-73
  *                         Mesh::loadMesh / Mesh::loadMtl    mesh.h:176-177, mesh.cpp:95-460
  *                         calculateNormals()                raytracing.h:41, raytracing.cpp:78-86
+ *   rt_scene_reserve      the rest of init()'s set-up: buffers for the first frame (raytracing.cpp:42-73)
  *   rt_scene_create       Mesh(vertices, triangles) ctor    mesh.h:175 (+ materials, mesh.h:197-200)
  *   rt_scene_destroy      (globals live for the process: main.cpp:17-18,130)
  *   rt_scene_export       read access to MyMesh / normals   raytracing.h:8, raytracing.cpp:33
@@ -213,6 +214,19 @@ int rt_render_tile(rt_scene *scene, const rt_params *params, int32_t x0, int32_t
 #define RT_SAMPLES_RAY_RGB 9
 int rt_trace_frame_samples(rt_scene *scene, const rt_params *params, int32_t layout, float *out, size_t capacity,
                            uint64_t counts[3]);
+/* Set-up without rendering: the render workspace of every pipeline a frame of params would use (tile_w x
+ * tile_h tiles over the whole frame; with RT_TUNE_FRAMES_IN_FLIGHT F, all F), and with samples_layout
+ * RT_SAMPLES_RGB / RT_SAMPLES_RAY_RGB the device staging of rt_trace_frame_samples. The first render of
+ * such a frame then allocates nothing (a host can do this in init(), raytracing.cpp:42-73, so the first
+ * 'r' press pays only the render). samples_layout 0: the workspace only. Synchronises the device's work
+ * on the scene's stream. */
+int rt_scene_reserve(rt_scene *scene, const rt_params *params, int32_t tile_w, int32_t tile_h, int32_t samples_layout);
+/* A stream (hipStream_t) on a hardware queue of its own, for hosts that keep frames in flight
+ * (RT_TUNE_FRAMES_IN_FLIGHT): two ordinary streams can land on one of the runtime's shared hardware
+ * queues (GPU_MAX_HW_QUEUES, 4 by default) and then run their frames one after the other. Pass it as
+ * the `stream` of the render entries; destroy it with rt_stream_destroy. */
+int  rt_stream_create(int32_t device, void **stream);
+void rt_stream_destroy(void *stream);
 /* Page-locked host memory (hipHostMalloc on the scene's device's runtime), for rt_trace_frame_samples'
  * output and other large device-to-host results. */
 int  rt_host_alloc(size_t bytes, void **out);

@@ -502,6 +502,21 @@ inline void calculateNormals() {
     for (size_t i = 0; i < nt; ++i) normals.push_back(Vec3Df(n[3 * i], n[3 * i + 1], n[3 * i + 2]));
 }
 
+namespace rtamd_dropin {
+// Pinned records for one 'r' frame's sub-samples (FrameCache::rec), grown when the frame grows.
+inline void ensure_records(float *&rec, size_t &cap, size_t floats) {
+    if (floats <= cap) return;
+    rt_host_free(rec);
+    rec = nullptr;
+    cap = 0;
+    void *m = nullptr;
+    check(rt_host_alloc(floats * sizeof(float), &m));
+    rec = static_cast<float *>(m);
+    cap = floats;
+}
+inline void reserve_frame();
+}  // namespace rtamd_dropin
+
 // init(char*), raytracing.cpp:42-73
 inline void init(char *fileName) {
     const char *path = fileName ? fileName : "cube.obj";
@@ -510,6 +525,7 @@ inline void init(char *fileName) {
     uploadMesh();
     calculateNormals();
     MyLightPositions.push_back(MyCameraPosition);   // light 0 = the camera position (:72)
+    rtamd_dropin::reserve_frame();
 }
 
 // isNullVector (raytracing.cpp:92-94)
@@ -620,6 +636,7 @@ struct FrameCache {
     size_t n = 0, next = 0;   // records in the frame; the next call's record
     float *rec = nullptr;     // 9 floats per sub-sample: origin, dest, rgb (pinned host memory)
     size_t rec_cap = 0;
+    size_t host_ray_frames = 0;   // frames whose records hold host-made rays (the host rounds differently)
     ~FrameCache() { rt_host_free(rec); }
     bool matches(const Vec3Df &o, const Vec3Df &d) const {   // the call's ray is record `next`'s, bit for bit
         uint32_t a[6], b[6];
@@ -658,22 +675,49 @@ inline bool start_frame(const Vec3Df &origin, const Vec3Df &dest) {
     FrameCache &fc = frame_cache();
     fc.n = fc.next = 0;
     const size_t n = static_cast<size_t>(WindowSize_X) * WindowSize_Y * pixelfactorX * pixelfactorY;
-    if (9 * n > fc.rec_cap) {
-        rt_host_free(fc.rec);
-        fc.rec = nullptr;
-        fc.rec_cap = 0;
-        void *m = nullptr;
-        check(rt_host_alloc(9 * n * sizeof(float), &m));
-        fc.rec = static_cast<float *>(m);
-        fc.rec_cap = 9 * n;
-    }
+    ensure_records(fc.rec, fc.rec_cap, 9 * n);
     rt_params p = params(max_lvl);
     for (int i = 0; i < 8; ++i)
         for (int k = 0; k < 3; ++k) p.corners[i][k] = c[i][k];
     check(rt_trace_frame_samples(scene(), &p, RT_SAMPLES_RAY_RGB, fc.rec, fc.rec_cap, nullptr));
     fc.state = TraceState::now();
     fc.n = n;
-    return fc.matches(origin, dest);   // (the device's first ray is the loop's: else the per-call path)
+    if (fc.matches(origin, dest)) return true;   // the device's first ray is the loop's
+    // The host's loop rounds differently from the device (e.g. built with FMA contraction: GCC's default
+    // -ffp-contract=fast on an FMA target). Make the frame's rays with loop_ray, compiled into this
+    // translation unit with the host's own flags like its loop, and trace exactly those in one call; the
+    // loop's calls then hit these records (a call whose ray still differs takes the per-call path).
+    std::vector<float> o(3 * n), d(3 * n), rgb(3 * n);
+    size_t k = 0;
+    for (unsigned y = 0; y < WindowSize_Y; ++y)
+        for (unsigned x = 0; x < WindowSize_X; ++x)
+            for (int sx = 0; sx < static_cast<int>(pixelfactorX); ++sx)
+                for (int sy = 0; sy < static_cast<int>(pixelfactorY); ++sy, ++k) {
+                    Vec3Df ro, rd;
+                    loop_ray(x, y, sx, sy, divX, divY, c, ro, rd);
+                    std::memcpy(&o[3 * k], ro.p, 12);
+                    std::memcpy(&d[3 * k], rd.p, 12);
+                }
+    check(rt_trace_rays(scene(), &p, o.data(), d.data(), static_cast<int32_t>(n), rgb.data(), nullptr));
+    ++fc.host_ray_frames;
+    for (k = 0; k < n; ++k) {
+        float *r = fc.rec + 9 * k;
+        std::memcpy(r, &o[3 * k], 12);
+        std::memcpy(r + 3, &d[3 * k], 12);
+        std::memcpy(r + 6, &rgb[3 * k], 12);
+    }
+    return fc.matches(origin, dest);
+}
+
+// The buffers of the first 'r' frame, made in init() (the reference's init loads the mesh; its first
+// 'r' press then pays only the trace): the render workspace and sample staging of a frame of the
+// current window and pixel factors (rt_scene_reserve) and the pinned records of its sub-samples.
+inline void reserve_frame() {
+    if (!scene() || WindowSize_X == 0 || WindowSize_Y == 0 || pixelfactorX == 0 || pixelfactorY == 0) return;
+    const rt_params p = params(max_lvl);
+    check(rt_scene_reserve(scene(), &p, 16, 16, RT_SAMPLES_RAY_RGB));
+    FrameCache &fc = frame_cache();
+    ensure_records(fc.rec, fc.rec_cap, 9 * static_cast<size_t>(WindowSize_X) * WindowSize_Y * pixelfactorX * pixelfactorY);
 }
 }  // namespace rtamd_dropin
 

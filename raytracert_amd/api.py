@@ -238,6 +238,12 @@ class Scene:
         check(lib().rt_trace_frame_samples(self._h, C.byref(p), layout, _ptr(rec), rec.size, _ptr(counts)))
         return rec, counts
 
+    def reserve(self, params: RenderParams | RtParams, tile_w: int = 16, tile_h: int = 16, samples_layout: int = 0):
+        """rt_scene_reserve: allocate what a frame of params needs (workspaces, sample staging) now,
+        so its first render allocates nothing."""
+        p = params.to_c() if isinstance(params, RenderParams) else params
+        check(lib().rt_scene_reserve(self._h, C.byref(p), tile_w, tile_h, samples_layout))
+
     def render_tiles_device(self, params: RenderParams | RtParams, tile_w: int, tile_h: int, first: int, stride: int,
                             out_ptr: int, out_capacity: int, stream_ptr: int | None = None, want_counts: bool = False,
                             frames: int = 1):
@@ -490,5 +496,17 @@ def device_count() -> int:
     return n.value
 
 
+def stream_create(device: int = 0) -> int:
+    """rt_stream_create: a hipStream_t (as an int) on a hardware queue of its own, for frames in
+    flight (wrap it with torch.cuda.ExternalStream); free it with stream_destroy."""
+    s = C.c_void_p()
+    check(lib().rt_stream_create(device, C.byref(s)))
+    return int(s.value)
+
+
+def stream_destroy(stream: int) -> None:
+    lib().rt_stream_destroy(C.c_void_p(stream))
+
+
 __all__ = ["Scene", "RenderParams", "Comm", "default_corners", "write_ppm", "device_count", "ray_intersect_triangle",
-           "assemble_tiles_device", "RT_HOST_ONLY"]
+           "assemble_tiles_device", "stream_create", "stream_destroy", "RT_HOST_ONLY"]

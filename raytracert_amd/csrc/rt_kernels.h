@@ -157,6 +157,11 @@ void launch_chain(const DevScene &s, const DevWork &w, const ShadeParams &p, int
                   hipStream_t stream, bool ordered = false, uint8_t *out_u8 = nullptr, float *out_f32 = nullptr,
                   int fuse_spp = 0, const FrameGeom *g = nullptr);
 void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t stream);
+// The chain kernels read their arguments through a struct view of the kernel-argument segment
+// (RT_OPAQUE_ARGS): a probe kernel with k_chain's parameter list checks that view against the bytes
+// the runtime packed for each argument. *bad = 0 when it matches, else the probe's word (bit k:
+// argument k of k_chain; *which = 0). Synchronises `stream`.
+hipError_t probe_chain_kernargs(hipStream_t stream, uint32_t *bad, int *which);
 // Batch order: the chain launch's wave batches sorted by the durations it measured, longest first
 // (w.batch_cost -> w.batch_order); the next launch over the same batches dispatches in that order
 // (launch_chain(..., ordered = true)). A counting sort: one fill and three small launches.

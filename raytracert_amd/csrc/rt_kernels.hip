@@ -19,6 +19,8 @@
 #include <algorithm>
 #include <cfloat>
 #include <cstdint>
+#include <cstring>
+#include <type_traits>
 
 #include "rt_kernels.h"
 #include "spec_pow.h"
@@ -1752,12 +1754,20 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
 // of batch order[s4 + ((vb - 4 s4) >> 1)]; later ones batch order[vb - 3 s4 - s2]. The host only
 // splits when a part holds whole pixels (launch_chain). Placement never changes results.
 // k_chain's explicit arguments as laid out in the kernel-argument segment (in order, each at its
-// natural alignment, as the members of a struct), for RT_OPAQUE_ARGS; k_chain checks the layout
-// against its own arguments at its start (a mismatch sets the error slot and ends the launch)
+// natural alignment, as the members of a struct), for RT_OPAQUE_ARGS. The layout is a property of
+// the kernel's signature, so it is checked once per kernel instantiation rather than per launch:
+// probe_chain_kernargs launches k_chain in probe mode (ordered -1), which compares every argument
+// with the ChainKernargs member at its place (chain_kernarg_mismatch) and reports a bit per argument.
+#ifndef RT_KARGS_PERTURB
+#define RT_KARGS_PERTURB 0   // test build only (librtamd_kargperturb.so): a layout the probe must reject
+#endif
 struct ChainKernargs {
     DevScene sc;
     ShadeParams p;
     DevWork w;
+#if RT_KARGS_PERTURB
+    int perturb;
+#endif
     int first, ordered;
     uint8_t *out_u8;
     float *out_f32;
@@ -1765,6 +1775,42 @@ struct ChainKernargs {
     FrameGeom g;
     int split, split8;
 };
+
+// Bit k set: argument k of k_chain is not where ChainKernargs places it. The probe launch fills each
+// by-value structure with a word pattern (word i of argument k = kKargTag[k] + i, padding included,
+// probe_chain_kernargs), so every word the struct view reads is checked against the bytes the
+// runtime packed for that argument; the scalars and pointers are compared with the formal values
+// (distinct sentinels). Bit 31 marks that the probe ran. (Taking the formals' addresses instead made
+// the compiler copy them into 736 B of scratch per lane.)
+constexpr uint32_t kKargTagScene = 0xA0000000u, kKargTagShade = 0xB0000000u, kKargTagWork = 0xC0000000u,
+                   kKargTagGeom = 0xD0000000u;
+template <typename T>
+__device__ __forceinline__ uint32_t karg_words_differ(const __attribute__((address_space(4))) T *m, uint32_t tag) {
+    const __attribute__((address_space(4))) uint32_t *u = (const __attribute__((address_space(4))) uint32_t *)m;
+    uint32_t bad = 0;
+    for (uint32_t i = 0; i < sizeof(T) / 4; ++i) bad |= static_cast<uint32_t>(u[i] != tag + i);
+    return bad;
+}
+__device__ __forceinline__ uint32_t chain_kernarg_mismatch(int first, int ordered, uint8_t *out_u8, float *out_f32, int fuse_spp,
+                                                           int spb, int nbatch, int split, int split8) {
+    typedef const __attribute__((address_space(4))) ChainKernargs *KargPtr;
+    const KargPtr ka = (KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
+    uint32_t bad = 0x80000000u;
+    bad |= karg_words_differ(&ka->sc, kKargTagScene) << 0;
+    bad |= karg_words_differ(&ka->p, kKargTagShade) << 1;
+    bad |= karg_words_differ(&ka->w, kKargTagWork) << 2;
+    bad |= static_cast<uint32_t>(ka->first != first) << 3;
+    bad |= static_cast<uint32_t>(ka->ordered != ordered) << 4;
+    bad |= static_cast<uint32_t>(ka->out_u8 != out_u8) << 5;
+    bad |= static_cast<uint32_t>(ka->out_f32 != out_f32) << 6;
+    bad |= static_cast<uint32_t>(ka->fuse_spp != fuse_spp) << 7;
+    bad |= static_cast<uint32_t>(ka->spb != spb) << 8;
+    bad |= static_cast<uint32_t>(ka->nbatch != nbatch) << 9;
+    bad |= karg_words_differ(&ka->g, kKargTagGeom) << 10;
+    bad |= static_cast<uint32_t>(ka->split != split) << 11;
+    bad |= static_cast<uint32_t>(ka->split8 != split8) << 12;
+    return bad;
+}
 template <int W, bool kAnyHit, bool kCount, bool kInLane = false, bool kSteal = false>
 __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kSteal ? RT_STEAL_WPE : RT_CHAIN_WPE))) void k_chain(
     const DevScene sc, const ShadeParams p, DevWork w, int first, int ordered, uint8_t *__restrict__ out_u8,
@@ -1779,7 +1825,10 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
 #endif
     for (int i = threadIdx.x; i < kChainSteps; i += kBvhBlock) { s_q[i] = 0; s_sh[i] = 0; }
 #if RT_OPAQUE_ARGS
-    {   // the argument layout ChainKernargs assumes: a mismatch is an internal error, not a result
+    {   // a per-launch spot check of six fields besides the load-time probe (k_chain_kernarg_probe checks
+        // every word): a mismatch sets the error slot and ends the launch. (A NaN corner is not one.
+        // Without this block the compiler allocates the kernel's registers differently: 28 instead of
+        // 24 B of spill per lane.)
         typedef const __attribute__((address_space(4))) ChainKernargs *KargPtr;
         const KargPtr ka = (KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
         if (ka->g.width != g.width || ka->p.n_lights != p.n_lights || ka->nbatch != nbatch || ka->split8 != split8 ||
@@ -2317,10 +2366,61 @@ int64_t chain_batches(int64_t capacity, int fuse_spp) {
 // k_chain's instantiations by width, any-hit shadows, work counting, fused frame and stealing
 typedef void (*ChainKernel)(const DevScene, const ShadeParams, DevWork, int, int, uint8_t *, float *, int, int, int,
                             const FrameGeom, int, int);
+// The layout probe: a kernel with exactly k_chain's parameter list (both are ChainKernel, checked
+// below), so its kernel-argument segment is laid out as every k_chain instantiation's. It runs
+// chain_kernarg_mismatch once. (Inside k_chain, even behind an early return, the check moved the
+// register allocation: spill 24 -> 36 B per lane.)
+__global__ __launch_bounds__(64) void k_chain_kernarg_probe(const DevScene sc, const ShadeParams p, DevWork w, int first, int ordered,
+                                                           uint8_t *__restrict__ out_u8, float *__restrict__ out_f32, int fuse_spp,
+                                                           int spb, int nbatch, const FrameGeom g, int split, int split8) {
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        *reinterpret_cast<uint32_t *>(out_u8) = chain_kernarg_mismatch(first, ordered, out_u8, out_f32, fuse_spp, spb, nbatch, split,
+                                                                       split8);
+}
+static_assert(std::is_same<decltype(&k_chain_kernarg_probe), ChainKernel>::value, "the probe must have k_chain's parameters");
+static_assert(std::is_same<decltype(&k_chain<4, true, false, true, false>), ChainKernel>::value, "k_chain's parameters changed");
+
 template <int W, bool kInLane, bool kSteal>
 ChainKernel chain_kernel(bool anyhit, bool count) {
     return anyhit ? (count ? k_chain<W, true, true, kInLane, kSteal> : k_chain<W, true, false, kInLane, kSteal>)
                   : (count ? k_chain<W, false, true, kInLane, kSteal> : k_chain<W, false, false, kInLane, kSteal>);
+}
+
+// k_chain_kernarg_probe once (one wave, tagged structures, sentinel scalars): *bad = its word unless
+// 0x80000000 (0: the layout matches ChainKernargs).
+hipError_t probe_chain_kernargs(hipStream_t stream, uint32_t *bad, int *which) {
+    *bad = 0;
+    *which = -1;
+    uint32_t *d = nullptr;
+    hipError_t e = hipMalloc(&d, sizeof(uint32_t));
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(d, 0, sizeof(uint32_t), stream);
+    // word i of each by-value argument = its tag + i (padding included): what the struct view must read
+    auto tagged = [](auto &obj, uint32_t tag) {
+        uint32_t wds[sizeof(obj) / 4];
+        for (uint32_t i = 0; i < sizeof(obj) / 4; ++i) wds[i] = tag + i;
+        std::memcpy(&obj, wds, sizeof(obj));
+    };
+    DevScene sc;
+    ShadeParams sp;
+    DevWork w;
+    FrameGeom g;
+    tagged(sc, kKargTagScene);
+    tagged(sp, kKargTagShade);
+    tagged(w, kKargTagWork);
+    tagged(g, kKargTagGeom);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_chain_kernarg_probe, dim3(1), dim3(64), 0, stream, sc, sp, w, 0x11, -1, reinterpret_cast<uint8_t *>(d),
+                           reinterpret_cast<float *>(static_cast<uintptr_t>(0x1234560)), 0x21, 0x31, 0x41, g, 0x51, 0x61);
+        e = hipGetLastError();
+    }
+    uint32_t h = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    const hipError_t ef = hipFree(d);
+    if (e != hipSuccess) return e;
+    if (h != 0x80000000u) { *bad = h ? h : 1u; *which = 0; }
+    return ef;
 }
 
 void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,

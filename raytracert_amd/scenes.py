@@ -188,3 +188,17 @@ def balls_surrogate(directory: str, stem: str = "balls_surrogate") -> str:
     with open(path, "w", newline="\n") as f:
         f.write("".join(lines))
     return path
+
+
+def orbit_corners(width: int, height: int, frame: int, step_deg: float = 0.25):
+    """Corner rays of view `frame` of an orbit: the reference's trackball (traqueboule.h:103-165) turned
+    by frame * step_deg degrees about the world y axis. main.cpp sets the modelview to T(0,0,-4) times
+    the trackball's rotation R (main.cpp:216-220), so produceRay's unprojected points (main.cpp:300-325)
+    are R^-1 applied to the default view's, about the world origin; MyCameraPosition stays the one
+    main.cpp:222 computed at start. Returns the 8 x 3 float32 corners (origin00, dest00, ..., dest11)."""
+    import numpy as np
+    from .api import default_corners
+    c = default_corners(width, height).astype(np.float64)
+    a = -np.deg2rad(frame * step_deg)
+    rot = np.array([[np.cos(a), 0.0, np.sin(a)], [0.0, 1.0, 0.0], [-np.sin(a), 0.0, np.cos(a)]])
+    return (c @ rot.T).astype(np.float32)

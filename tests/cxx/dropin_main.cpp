@@ -289,6 +289,7 @@ int main(int argc, char **argv) {
             render_one_call();
         } else if (k[0] == 'T') {
             render_r(true);
+            std::printf("cache host_ray_frames %zu\n", rtamd_dropin::frame_cache().host_ray_frames);
         } else if (k[0] == 'H') {
             render_host_floor();
         } else if (k[0] == 'P' && k[1] == ':') {   // single calls off the frame cache (rays of no frame)

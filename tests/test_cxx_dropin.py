@@ -211,3 +211,22 @@ def test_dropin_mesh_texcoords_and_loadmtl(dropin_bin, workdir, tmp_path):
     assert mt[2][3] == _bits(0.25) and mt[0][4] == _bits(10.0)
     lines = _lines([dropin_bin, "host", path, str(tmp_path / "missing.mtl")])
     assert next(l for l in lines if l.startswith("loadmtl ")).split()[1:3] == ["0", "0"]
+
+
+@pytest.mark.gpu
+def test_dropin_loop_with_fma_contraction_still_uses_frame_trace(workdir, tmp_path, gpu_available):
+    """a host built with GCC's default -ffp-contract=fast on an FMA target makes the 'r'
+    loop's rays with FMAs, so they differ from the device's (which follow the reference's x86-64 build,
+    no FMA). The drop-in then traces the loop's own rays, made by the header's loop_ray in the host's
+    translation unit, in one call: the literal loop still takes well under a second (the per-call path
+    would take minutes), its frame records say so, and the frame is the one-call frame's up to the
+    few pixels whose rays round differently."""
+    exe = _build(str(tmp_path / "dropin_fma"), ["-mfma", "-ffp-contract=fast", "-I" + os.path.join(ROOT, "include")])
+    path = scene_path("ref:dodgeColorTest.obj", workdir)
+    lines = _lines([exe, "keys", path, "500", "500", str(tmp_path / "c"), "T", "T", "R"])
+    fr = [l.split() for l in lines if l.startswith("frame ")]
+    cache = [int(l.split()[2]) for l in lines if l.startswith("cache host_ray_frames")]
+    assert float(fr[1][10]) < 5000.0, fr[1]
+    assert cache[-1] >= 1, "the FMA build's rays matched the device's: this test no longer covers the fallback"
+    loop, one = read_ppm(fr[1][1]), read_ppm(fr[2][1])
+    assert (loop == one).mean() >= 0.999

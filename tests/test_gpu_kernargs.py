@@ -1,0 +1,93 @@
+"""The chain kernel's kernel-argument view (RT_OPAQUE_ARGS, VERDICT r04 "weak" 9).
+
+k_chain reads its ~190 argument words through a struct view of the kernel-argument segment
+(ChainKernargs). At scene upload the library runs k_chain_kernarg_probe once per device: a kernel
+with k_chain's parameter list (a static_assert pins the two signatures together) that compares
+every word of every by-value argument, as the struct view reads it, with the tagged pattern the host
+packed (rt_kernels.hip chain_kernarg_mismatch). A test build whose ChainKernargs is shifted by one
+int (RT_KARGS_PERTURB, raytracert_amd/build/librtamd_kargperturb.so, built by the Makefile) must be
+refused at load with RT_E_HIP, and the real build must load.
+
+The per-launch spot check inside k_chain compares a camera corner as a float (NaN != NaN would
+misfire): frames whose corner rays hold NaN must render (not RT_E_HIP) and equal the oracle's.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle as O
+import raytracert_amd as R
+from raytracert_amd import scenes
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+PERTURBED = os.path.join(ROOT, "raytracert_amd", "build", "librtamd_kargperturb.so")
+
+LOAD_SCRIPT = r"""
+import sys
+sys.path.insert(0, {root!r})
+import raytracert_amd as R
+from raytracert_amd import scenes
+obj = scenes.write_sphere_grid(scenes.F4, {d!r}, "karg")
+try:
+    with R.Scene.load(obj, device=0) as sc:
+        u8, _, counts = sc.render(R.RenderParams(width=32, height=16, pf=1, max_lvl=1))
+    print("LOADED", int(sum(counts)))
+except Exception as e:
+    print("REFUSED", e)
+"""
+
+
+def _load_with(lib, d):
+    env = dict(os.environ)
+    env.pop("RTAMD_LIB", None)
+    if lib:
+        env["RTAMD_LIB"] = lib
+    r = subprocess.run([sys.executable, "-c", LOAD_SCRIPT.format(root=ROOT, d=d)], env=env, capture_output=True, text=True,
+                       timeout=300)
+    return r.stdout + r.stderr
+
+
+def test_perturbed_build_exists():
+    """build() makes the test build next to the product (its probe is what the GPU test exercises)."""
+    assert os.path.exists(PERTURBED), "make -C raytracert_amd builds build/librtamd_kargperturb.so"
+
+
+@pytest.mark.gpu
+def test_perturbed_kernarg_layout_is_refused(tmp_path, gpu_available):
+    out = _load_with(PERTURBED, str(tmp_path))
+    assert "REFUSED" in out and "ChainKernargs" in out, out
+    out = _load_with(None, str(tmp_path))
+    assert "LOADED" in out, out
+
+
+def _nan_params(which, width=48, height=27, pf=1, max_lvl=3):
+    cs = R.default_corners(width, height).copy()
+    cs[which] = np.float32(np.nan)
+    lights = [[0.0, 0.0, 4.0], [1.5, 1.5, 4.0]]
+    p = R.RenderParams(width=width, height=height, pf=pf, max_lvl=max_lvl, lights=lights, corners=cs)
+    op = O.make_params(width, height, pf, max_lvl, lights=lights, corners=cs)
+    return p, op
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", [(7, 2), (1, 0), (0, 1)])
+def test_nan_corner_frame_matches_oracle(which, tmp_path, gpu_available):
+    """corners[7][2] (the value the spot check compares), a dest and an origin component as NaN:
+    the fused chain launch renders the frame, and it equals the CPU restatement's."""
+    obj = scenes.write_sphere_grid(scenes.F4, str(tmp_path), "nan")
+    p, op = _nan_params(which)
+    with R.Scene.load(obj, device=0) as sc:
+        u8, _, counts = sc.render(p)
+        import torch
+        buf = torch.zeros(p.height * p.width * 3, dtype=torch.uint8, device="cuda:0")
+        sc.render_frame_device(p, 16, 16, buf.data_ptr(), buf.numel(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        fd = buf.cpu().numpy().reshape(p.height, p.width, 3)
+    _, ou8, oc = O.OracleScene(obj).render(op)
+    assert [int(c) for c in counts] == [int(c) for c in oc]
+    assert np.array_equal(u8, ou8)
+    assert np.array_equal(fd, ou8)
