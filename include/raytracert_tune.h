@@ -111,6 +111,13 @@ extern "C" {
                                     pipeline's own stream (forked from the caller's stream and joined back),
                                     so two frames in flight overlap whichever hardware queues the caller's
                                     streams share; 0 (default): on the caller's stream. Placement only */
+#define RT_TUNE_QUAD_WALK 35      /* 1: the waves of the quarter tier (RT_TUNE_STEAL_QUARTER) walk with four lanes
+                                    per ray: lane q of a quad tests child q of each four-wide node and a
+                                    leaf's triangles side by side, so a ray's node visit costs ~60 instead of
+                                    ~130 wave-instructions and the longest chains of the frame (its critical
+                                    path) finish sooner; a part then holds at most 16 samples of whole pixels
+                                    (pf 1, 2, 4; otherwise the plain quarter tier). 0 (default): off.
+                                    Placement only */
 #define RT_TUNE_TOP_NODES 13     /* retired in r03 (0-85 accepted, no effect): an LDS copy of the four-wide
                                     tree's top levels; with float node rows loaded from global memory it
                                     measured slower (flat loads, 64-bit addresses) */

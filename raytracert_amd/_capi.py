@@ -51,6 +51,7 @@ TUNE_FRAMES_IN_FLIGHT = 31
 TUNE_ADOPT_ORDER = 32
 TUNE_INFLIGHT_DYNAMIC = 33
 TUNE_INFLIGHT_STREAMS = 34
+TUNE_QUAD_WALK = 35
 BVH_INFO_FIELDS = 7
 STOCHASTIC = 1 << 8
 DEFAULT_SEED = 0x5EED

@@ -96,6 +96,7 @@ struct DevScene {
     int32_t dyn_group_log2;         // RT_TUNE_DYN_GROUP: log2 of the consecutive wave tasks dealt to one XCD
     int32_t prio_batches;           // RT_TUNE_PRIORITY_BATCHES: longest batches run at raised wave priority
     int32_t shadow_helpers;         // RT_TUNE_SHADOW_HELPERS: split waves' idle lanes walk their owners' lights
+    int32_t quad_walk;              // RT_TUNE_QUAD_WALK: the quarter tier's waves walk with four lanes per ray
 };
 
 struct DevWork {

@@ -864,6 +864,182 @@ __device__ __forceinline__ void bvh4_query_steal(const DevScene &sc, V3 o, V3 di
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Quad walk (RT_TUNE_QUAD_WALK, the quarter tier of ordered launches, r05): four lanes per ray. The
+// four lanes of a quad hold the same ray, its stack and its chain; lane q of the quad tests child q
+// of each four-wide node (one box, not four), the quad ranks the four entry distances with DPP lane
+// exchanges, the nearest wanted child is visited next and the others are pushed by their own lanes;
+// a leaf's triangles are tested side by side (lane q: triangle q, q + 4, ...). A node visit is then
+// ~60 wave-instructions instead of ~130, so a ray's walk, bound by the dependent issue and load
+// latency of its visits, shortens: this is for the longest batches of the order (the frame's
+// critical path), whose every lane carries three reflections. Exactness: the node test per child is
+// the per-lane walk's (the same te/tx/tcull arithmetic), the cull bound is the quad's least accepted
+// distance (a hit of this ray), every triangle of every visited leaf is tested by one lane, and the
+// result is the lexicographic (distance, index) minimum over the quad's lanes: the same minimum as
+// any other order of the same tests. Every DPP exchange below runs with all four lanes of each
+// active quad active (the quad's control flow is uniform: all its values are the same).
+// ---------------------------------------------------------------------------------------------
+constexpr int kQuadSamples = kWaveBatch / 4;   // samples (quads) per wave in the quad walk
+__device__ __forceinline__ int dpp_qx1(int v) { return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false); }   // lane ^ 1
+__device__ __forceinline__ int dpp_qx2(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false); }   // lane ^ 2
+__device__ __forceinline__ int dpp_qx3(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x1B, 0xF, 0xF, false); }   // lane ^ 3
+__device__ __forceinline__ float quad_min(float x) {
+    x = fminf(x, as_float(dpp_qx1(as_int(x))));
+    return fminf(x, as_float(dpp_qx2(as_int(x))));
+}
+__device__ __forceinline__ bool quad_any(bool b) {
+    int v = static_cast<int>(b);
+    v |= dpp_qx1(v);
+    v |= dpp_qx2(v);
+    return v != 0;
+}
+// The lexicographic (distance, index) minimum over the quad, with its point, in every lane. A lane
+// without a hit holds (FLT_MAX, -1): any hit is below FLT_MAX (test_triangle accepts dist < best).
+__device__ __forceinline__ void quad_lex_min(float &best, int &bidx, V3 &bI) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const float ob = as_float(r ? dpp_qx2(as_int(best)) : dpp_qx1(as_int(best)));
+        const int oi = r ? dpp_qx2(bidx) : dpp_qx1(bidx);
+        const float ox = as_float(r ? dpp_qx2(as_int(bI.x)) : dpp_qx1(as_int(bI.x)));
+        const float oy = as_float(r ? dpp_qx2(as_int(bI.y)) : dpp_qx1(as_int(bI.y)));
+        const float oz = as_float(r ? dpp_qx2(as_int(bI.z)) : dpp_qx1(as_int(bI.z)));
+        const bool take = ob < best || (ob == best && static_cast<uint32_t>(oi) < static_cast<uint32_t>(bidx));
+        best = take ? ob : best;
+        bidx = take ? oi : bidx;
+        bI = take ? mk(ox, oy, oz) : bI;
+    }
+}
+
+// A quad's traversal stack: its wave's 16 x 64 words of the block's lane stacks (LaneStack rows
+// [entry][lane], this wave's 64 columns) seen as 64 entries x 16 quads; deeper entries in the global
+// overflow area at the quad's first lane ([entry - cap][grid lane], inside the per-lane area).
+struct QuadStack {
+    int32_t *lds;   // this wave's first column of row 0
+    int32_t *ovf;
+    int cap, stride, gl0, slot;
+    __device__ __forceinline__ int32_t *at_lds(int e) const { return lds + (e >> 2) * kBvhBlock + ((e & 3) << 4) + slot; }
+    __device__ __forceinline__ void put(int e, int32_t v) const {
+        if (e < cap) *at_lds(e) = v;
+        else ovf[static_cast<size_t>(e - cap) * stride + gl0] = v;
+    }
+    __device__ __forceinline__ int32_t get(int e) const {
+        int32_t v = *at_lds(min(e, cap - 1));
+        if (e >= cap) v = ovf[static_cast<size_t>(e - cap) * stride + gl0];
+        return v;
+    }
+};
+__device__ __forceinline__ QuadStack quad_stack(const DevScene &sc, int32_t *lds) {
+    QuadStack st;
+    const int lane = static_cast<int>(threadIdx.x) & 63, wbase = static_cast<int>(threadIdx.x) & ~63;
+    st.lds = lds + wbase;
+    st.ovf = sc.stack_ovf;
+    st.cap = 4 * sc.lds_stack;
+    st.stride = static_cast<int>(gridDim.x) * kBvhBlock;
+    st.gl0 = static_cast<int>(blockIdx.x) * kBvhBlock + wbase + (lane & ~3);
+    st.slot = lane >> 2;
+    return st;
+}
+
+// One node visit of the quad walk: returns the next ref (the nearest wanted child, else the stack
+// top, else kDoneRef) in every lane of the quad. q = this lane's child slot, qshift = the quad's
+// first lane (its bits in a ballot).
+template <bool kAnyHit>
+__device__ __forceinline__ int32_t node4_next_quad(const Ray4 &R, const Bvh4F *__restrict__ nodes4, int32_t node, const QuadStack &st,
+                                                   int &sp, int q, int qshift) {
+    const char *__restrict__ base = reinterpret_cast<const char *>(nodes4);
+    const uint32_t o = static_cast<uint32_t>(node) * static_cast<uint32_t>(sizeof(Bvh4F)) + 4u * static_cast<uint32_t>(q);
+    const float nx = *reinterpret_cast<const float *>(base + (o + R.rows[0]));
+    const float ny = *reinterpret_cast<const float *>(base + (o + R.rows[1]));
+    const float nz = *reinterpret_cast<const float *>(base + (o + R.rows[2]));
+    const float fx = *reinterpret_cast<const float *>(base + (o + R.rows[3]));
+    const float fy = *reinterpret_cast<const float *>(base + (o + R.rows[4]));
+    const float fz = *reinterpret_cast<const float *>(base + (o + R.rows[5]));
+    const int32_t ref = *reinterpret_cast<const int32_t *>(base + (o + static_cast<uint32_t>(offsetof(Bvh4F, child))));
+    const float tnx = fmaf(nx, R.ax.x, R.ax.y), tfx = fmaf(fx, R.ax.x, R.fxy.x);
+    const float tny = fmaf(ny, R.ay.x, R.ay.y), tfy = fmaf(fy, R.ay.x, R.fxy.y);
+    const float tnz = fmaf(nz, R.az.x, R.az.y), tfz = fmaf(fz, R.az.x, R.fzc.x);
+    const float te = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), 0.0f);
+    const float tx = fminf(fminf(tfx, tfy), tfz);
+    const bool want = te <= node_lim<kAnyHit>(tx, R.fzc.y);   // (the per-lane walk's test for this child)
+    // rank among the quad by entry distance: te >= 0, so its bits order as the floats; the two low
+    // bits (the slot) break ties and make the keys distinct (traversal order only); misses sort last
+    const uint32_t key = want ? ((static_cast<uint32_t>(as_int(te)) & ~3u) | static_cast<uint32_t>(q)) : (0xFFFFFFFCu | static_cast<uint32_t>(q));
+    const uint32_t k1 = static_cast<uint32_t>(dpp_qx1(static_cast<int>(key)));
+    const uint32_t k2 = static_cast<uint32_t>(dpp_qx2(static_cast<int>(key)));
+    const uint32_t k3 = static_cast<uint32_t>(dpp_qx3(static_cast<int>(key)));
+    const int rank = static_cast<int>(k1 < key) + static_cast<int>(k2 < key) + static_cast<int>(k3 < key);
+    const int nh = __popc(static_cast<uint32_t>(__ballot(want) >> qshift) & 0xFu);
+    int32_t r0 = rank == 0 ? ref : 0;   // the nearest child's ref, to every lane of the quad
+    r0 += dpp_qx1(r0);
+    r0 += dpp_qx2(r0);
+    if (want && rank > 0) st.put(sp + nh - 1 - rank, ref);   // farthest deepest: rank 1 ends on top
+    sp += max(nh - 1, 0);
+    if (nh > 0) return r0;
+    if (sp <= 0) return kDoneRef;
+    return st.get(--sp);
+}
+
+// The always-tested list split over the quad's lanes (lane q: entries q, q + 4, ...).
+template <bool kAnyHit>
+__device__ __forceinline__ void test_always_quad(const DevScene &sc, V3 o, V3 dir, float &best, int &bidx, V3 &bI, bool &done, int q) {
+    for (int i = q; i < sc.n_always; i += 4)
+        test_triangle<kAnyHit, true, RT_ALWAYS_SIGN>(sc.always_recs[i], static_cast<int>(sc.always[i]), o, dir, best, bidx, bI, done);
+}
+
+template <bool kAnyHit>
+__device__ __forceinline__ void bvh4_query_quad(const DevScene &sc, V3 o, V3 dir, bool active, int &bidx, V3 &bI,
+                                                const QuadStack &st, unsigned &tests, unsigned &visits, int q, int qshift) {
+    float best = FLT_MAX;
+    bool done = !active;
+    test_always_quad<kAnyHit>(sc, o, dir, best, bidx, bI, done, q);
+    if (active && !(kAnyHit && quad_any(done))) {
+        Ray4 R;
+        float pad;
+        ray4_setup(sc, o, dir, R, pad);
+        if (!kAnyHit) {
+            const float qb = quad_min(best);
+            if (qb < FLT_MAX) R.fzc.y = cull_param(R, qb, pad);
+        }
+        int sp = 0;
+        int32_t node = 0, leaf = kDoneRef;
+        while (true) {
+            while (node >= 0) {
+                if (q == 0) ++visits;
+                node = node4_next_quad<kAnyHit>(R, sc.nodes4f, node, st, sp, q, qshift);
+                if (node < 0 && node != kDoneRef && leaf == kDoneRef) {   // postpone the leaf, keep walking
+                    leaf = node;
+                    node = sp > 0 ? st.get(--sp) : kDoneRef;
+                }
+                if (__all(leaf != kDoneRef)) break;   // every quad still walking holds a leaf
+            }
+            while (leaf != kDoneRef) {   // one leaf per iteration: its triangles side by side
+                const uint32_t u = static_cast<uint32_t>(leaf);
+                const int cnt = static_cast<int>((u >> kBvhCountShift) & kBvhCountMask);
+                const int first = static_cast<int>(u & ((1u << kBvhCountShift) - 1u));
+                for (int k = q; k < cnt; k += 4) {
+                    test_triangle<kAnyHit, true, RT_LEAF_SIGN>(leaf_rec(sc, first + k), static_cast<int>(sc.leaf_idx[first + k]), o, dir,
+                                                               best, bidx, bI, done);
+                    ++tests;
+                }
+                if (kAnyHit) {
+                    if (quad_any(done)) { node = kDoneRef; leaf = kDoneRef; break; }
+                } else {
+                    const float qb = quad_min(best);
+                    if (qb < FLT_MAX) R.fzc.y = cull_param(R, qb, pad);
+                }
+                leaf = kDoneRef;
+                if (node < 0 && node != kDoneRef) {
+                    leaf = node;
+                    node = sp > 0 ? st.get(--sp) : kDoneRef;
+                }
+            }
+            if (node == kDoneRef) break;
+        }
+    }
+    quad_lex_min(best, bidx, bI);
+    if (bidx < 0) bI = mk(0, 0, 0);
+}
+
 
 // The closest-hit / any-hit query of the tree kernels: W = 4 the four-wide while-while walk (or,
 // kSteal, its in-wave stealing form), W = 2 the binary tree (scenes above 1e6 in magnitude).
@@ -1728,6 +1904,38 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
     return shade_hit<kInLane, false>(sc, p, w, step, sample, ray, lvl, bidx, bI, [&](int l) { return ((mask >> l) & 1u) != 0; });
 }
 
+// chain_step for a quad (the quad walk): the four lanes hold the same sample and ray and run the same
+// shading (each writes the same chain record); the closest-hit and every light's shadow query are
+// quad walks. Ray statistics and work counts come from lane q == 0 (tests from the lane that ran each).
+template <bool kAnyHit, bool kCount>
+__device__ __forceinline__ Secondary chain_step_quad(const DevScene &sc, const ShadeParams &p, const DevWork &w, int step, int sample,
+                                                     V3 org, V3 dst, int lvl, const QuadStack &st, int *s_sh, WorkTally<kCount> &wc,
+                                                     WorkTally<kCount> &ws, int q, int qshift) {
+    Secondary none;
+    none.state = kChildNone;
+    none.local = mk(0, 0, 0);   // trace() miss: black (:389-391)
+    int bidx = -1;
+    V3 bI = mk(0, 0, 0);
+    const V3 ray = sub(dst, org);
+    bvh4_query_quad<false>(sc, org, ray, true, bidx, bI, st, wc.tests, wc.visits, q, qshift);
+    if (bidx >= sc.nt) { w.counters[kErrorSlot] = 1; bidx = -1; }
+    if (bidx < 0) return none;
+    uint32_t mask = 0;   // isShadow per light (:241-261)
+    if ((p.flags & RT_SHADOWS) && p.n_lights > 0) {
+        if (q == 0) atomicAdd(&s_sh[step], p.n_lights);
+        const V3 so = mk(bI.x + 0.1f, bI.y + 0.1f, bI.z + 0.1f);                // :248
+        for (int l = 0; l < p.n_lights; ++l) {
+            int sidx = -1;
+            V3 sI = mk(0, 0, 0);
+            const V3 Lp = light_at<false>(p.lights, p.light_ext, l);
+            const V3 sd = mk(Lp.x - so.x, Lp.y - so.y, Lp.z - so.z);
+            bvh4_query_quad<kAnyHit>(sc, so, sd, true, sidx, sI, st, ws.tests, ws.visits, q, qshift);
+            if (sidx >= 0 && !sc.mats[sc.tri_mat[sidx]].transparent) mask |= 1u << l;   // :253-257
+        }
+    }
+    return shade_hit<true, false>(sc, p, w, step, sample, ray, lvl, bidx, bI, [&](int l) { return ((mask >> l) & 1u) != 0; });
+}
+
 // The chain launch: steps first..max_lvl of every query, each lane carrying its own ray through
 // closest-hit, its shadow rays and shade until its chain ends. With no launch boundary between
 // steps, a lane's next step does not wait for the slowest wave of the current one, which is what
@@ -1753,6 +1961,63 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
 // vb < 4 s4 is quarter vb & 3 of batch order[vb >> 2]; then vb - 4 s4 < 2 s2 is half (vb - 4 s4) & 1
 // of batch order[s4 + ((vb - 4 s4) >> 1)]; later ones batch order[vb - 3 s4 - s2]. The host only
 // splits when a part holds whole pixels (launch_chain). Placement never changes results.
+// One part of a quarter-tier batch as a quad walk (RT_TUNE_QUAD_WALK): samples j0 .. j0 + n - 1, sample
+// j0 + lane / 4 on the four lanes of a quad, each lane making the same primary ray, chain and fold;
+// then the part's whole pixels are summed in sub-sample order across quads (k_frame's arithmetic) and
+// written by the pixel's first quad's lane 0. n <= kQuadSamples (the host enables the tier only then).
+template <bool kAnyHit, bool kCount>
+__device__ __forceinline__ void quad_batch(const DevScene &sc, const ShadeParams &p, const DevWork &w, const FrameGeom &g, int32_t *lds_stack,
+                                           int *s_q, int *s_sh, WorkTally<kCount> &wc, WorkTally<kCount> &ws, uint8_t *out_u8,
+                                           float *out_f32, int spp, int j0, int n, int nq) {
+    const int lane = __lane_id(), sl = lane >> 2, q = lane & 3, qshift = lane & ~3;
+    const QuadStack st = quad_stack(sc, lds_stack);
+    const int j = j0 + sl;
+    V3 rgb = mk(0, 0, 0);
+    int px = -1;
+    if (sl < n && j < nq) {
+        V3 org, dst;
+        int64_t pxi = 0;
+        int sub = 0;
+        if (!primary_sample(g, j, org, dst, pxi, sub)) {
+            if (g.out_mode == 0 && out_u8 && sub == 0 && q == 0) { out_u8[3 * pxi] = 0; out_u8[3 * pxi + 1] = 0; out_u8[3 * pxi + 2] = 0; }
+        } else {
+            px = g.out_mode == 2 ? static_cast<int>(pxi) * spp + sub : static_cast<int>(pxi);
+            if (g.out_mode == 2 && g.sample_stride == 9 && q == 0) {   // the record's ray (RT_SAMPLES_RAY_RGB)
+                float *r = out_f32 + 9 * static_cast<int64_t>(px);
+                r[0] = org.x; r[1] = org.y; r[2] = org.z; r[3] = dst.x; r[4] = dst.y; r[5] = dst.z;
+            }
+            int lvl = 0;
+            for (int step = 0; step < kChainSteps; ++step) {
+                if (step > 0 && q == 0) atomicAdd(&s_q[step], 1);
+                const Secondary sec = chain_step_quad<kAnyHit, kCount>(sc, p, w, step, j, org, dst, lvl, st, s_sh, wc, ws, q, qshift);
+                if (sec.state != kChildTrace) {   // the chain ends here: fold it (fold_chain's arithmetic)
+                    rgb = fold_inlane(sc, w, 0, step, j, sec.state == kChildZero ? add(sec.local, mk(0.0f, 0.0f, 0.0f)) : sec.local);
+                    break;
+                }
+                org = sec.org;
+                dst = sec.dst;
+                lvl = sec.lvl;
+            }
+        }
+    }
+    if (g.out_mode == 2) {   // every sub-sample's own colour (rt_trace_frame_samples)
+        if (px >= 0 && q == 0) {
+            float *o = out_f32 + static_cast<int64_t>(g.sample_stride) * px + (g.sample_stride - 3);
+            o[0] = rgb.x; o[1] = rgb.y; o[2] = rgb.z;
+        }
+        return;
+    }
+    const int pix_sl = sl - sl % spp;   // the pixel's first sub-sample's quad
+    V3 acc = mk(0, 0, 0);
+    for (int sub = 0; sub < spp; ++sub) {   // summed in sub-sample order (main.cpp:377-391)
+        const int src = min(pix_sl + sub, kQuadSamples - 1) * 4;
+        acc = add(acc, mk(__shfl(rgb.x, src), __shfl(rgb.y, src), __shfl(rgb.z, src)));
+    }
+    const float div = static_cast<float>(spp);
+    acc = mk(acc.x / div, acc.y / div, acc.z / div);   // operator/, Vec3D.h:36-38
+    if (sl == pix_sl && q == 0 && px >= 0) store_pixel(acc, 3 * static_cast<int64_t>(px), out_u8, out_f32);
+}
+
 // k_chain's explicit arguments as laid out in the kernel-argument segment (in order, each at its
 // natural alignment, as the members of a struct), for RT_OPAQUE_ARGS. The layout is a property of
 // the kernel's signature, so it is checked once per kernel instantiation rather than per launch:
@@ -1811,7 +2076,7 @@ __device__ __forceinline__ uint32_t chain_kernarg_mismatch(int first, int ordere
     bad |= static_cast<uint32_t>(ka->split8 != split8) << 12;
     return bad;
 }
-template <int W, bool kAnyHit, bool kCount, bool kInLane = false, bool kSteal = false>
+template <int W, bool kAnyHit, bool kCount, bool kInLane = false, bool kSteal = false, bool kQuad = false>
 __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kSteal ? RT_STEAL_WPE : RT_CHAIN_WPE))) void k_chain(
     const DevScene sc, const ShadeParams p, DevWork w, int first, int ordered, uint8_t *__restrict__ out_u8,
     float *__restrict__ out_f32, int fuse_spp, int spb, int nbatch, const FrameGeom g, int split, int split8) {
@@ -1910,6 +2175,15 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         int px = -1;   // (out_mode 2: the sample's output slot, pixel x spp + sub-sample)
         // shadow helpers (RT_TUNE_SHADOW_HELPERS): in a split wave of the fused launch the lanes past
         // the part's plen samples help their owners' shadow walks, roles = lanes per sample (<= lights)
+        // the quad walk (RT_TUNE_QUAD_WALK): a quarter-tier part's samples on four lanes each
+        // (its own instantiation, kQuad: compiled into the default kernel the quad path's registers moved the
+        // per-lane path's allocation from 24 to 92 B of spill per lane)
+        const bool quad = kQuad && kInLane && !kSteal && W == 4 && nparts == 4 && scb.quad_walk && plen <= kQuadSamples;
+        if (quad) {
+            if (wave_on)
+                quad_batch<kAnyHit, kCount>(scb, pl, wb, gl, lds_stack, s_q, s_sh, wc, ws, out_u8, out_f32, fuse_spp,
+                                            pb * spb + part * plen, min(plen, spb - part * plen), nq);
+        } else {
         const int roles = (kInLane && !kSteal && nparts > 1 && scb.shadow_helpers && (pl.flags & RT_SHADOWS))
                               ? max(1, min(kWave / plen, pl.n_lights)) : 1;
         const int role = (roles > 1 && lane >= plen && lane < roles * plen) ? lane / plen : 0;
@@ -1978,6 +2252,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
             const float div = static_cast<float>(fuse_spp);
             acc = mk(acc.x / div, acc.y / div, acc.z / div);   // operator/, Vec3D.h:36-38
             if (lane == pix_lane && px >= 0) store_pixel(acc, 3 * static_cast<int64_t>(px), out_u8, out_f32);
+        }
         }
         // the batch's lifetime (a split batch: its parts' lifetimes, the last to finish stored), with
         // bit 31 set for a split batch (kCostSplit): the sort counts it double, so a batch that ran
@@ -2380,10 +2655,10 @@ __global__ __launch_bounds__(64) void k_chain_kernarg_probe(const DevScene sc, c
 static_assert(std::is_same<decltype(&k_chain_kernarg_probe), ChainKernel>::value, "the probe must have k_chain's parameters");
 static_assert(std::is_same<decltype(&k_chain<4, true, false, true, false>), ChainKernel>::value, "k_chain's parameters changed");
 
-template <int W, bool kInLane, bool kSteal>
+template <int W, bool kInLane, bool kSteal, bool kQuad = false>
 ChainKernel chain_kernel(bool anyhit, bool count) {
-    return anyhit ? (count ? k_chain<W, true, true, kInLane, kSteal> : k_chain<W, true, false, kInLane, kSteal>)
-                  : (count ? k_chain<W, false, true, kInLane, kSteal> : k_chain<W, false, false, kInLane, kSteal>);
+    return anyhit ? (count ? k_chain<W, true, true, kInLane, kSteal, kQuad> : k_chain<W, true, false, kInLane, kSteal, kQuad>)
+                  : (count ? k_chain<W, false, true, kInLane, kSteal, kQuad> : k_chain<W, false, false, kInLane, kSteal, kQuad>);
 }
 
 // k_chain_kernarg_probe once (one wave, tagged structures, sentinel scalars): *bad = its word unless
@@ -2435,9 +2710,6 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
     // resident waves, where a few long walks set the frame time): four-wide, fused launches
     const int64_t resident_lanes = static_cast<int64_t>(std::max(s.resident_grid, 1)) * kBvhBlock;
     const bool steal = wide && fused && (s.wave_steal == 1 || (s.wave_steal == 2 && capacity <= 2 * resident_lanes));
-    ChainKernel k = steal  ? chain_kernel<4, true, true>(anyhit, count)
-                  : fused  ? (wide ? chain_kernel<4, true, false>(anyhit, count) : chain_kernel<2, true, false>(anyhit, count))
-                           : (wide ? chain_kernel<4, false, false>(anyhit, count) : chain_kernel<2, false, false>(anyhit, count));
     const int spb = fused ? chain_spb(fuse_spp) : kWave;
     const int64_t nbatch = fused ? chain_batches(capacity, fuse_spp) : (capacity + kWave - 1) / kWave;
     // ordered launches over grid-stride batches: the longest batches run as eighth, quarter and half
@@ -2452,6 +2724,13 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
         if (ppb >= 4) { s4 = static_cast<int>(std::min<int64_t>(cap, s.steal_quarter)); cap -= s4; }
         if (ppb >= 2) s2 = static_cast<int>(std::min<int64_t>(cap, s.steal_half));
     }
+    // the quarter tier as quad walks (RT_TUNE_QUAD_WALK) when a quarter holds at most 16 samples
+    const int ppb_f = fused ? spb / fuse_spp : 0;
+    const bool quad = wide && fused && !steal && s.quad_walk && s4 > 0 && ((ppb_f + 3) / 4) * fuse_spp <= kQuadSamples;
+    ChainKernel k = steal  ? chain_kernel<4, true, true>(anyhit, count)
+                  : quad   ? chain_kernel<4, true, false, true>(anyhit, count)
+                  : fused  ? (wide ? chain_kernel<4, true, false>(anyhit, count) : chain_kernel<2, true, false>(anyhit, count))
+                           : (wide ? chain_kernel<4, false, false>(anyhit, count) : chain_kernel<2, false, false>(anyhit, count));
     const int split = s2 | (s4 << 16);
     const FrameGeom geom = g ? with_divisors(*g) : FrameGeom{};
     // distribution 4 (dynamic wave tasks): a resident grid, each wave takes tasks until none remain

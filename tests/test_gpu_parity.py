@@ -513,6 +513,33 @@ def test_split_batches_match_plain_walk(spec, w, h, pf, pfy, steal, half, quarte
             assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32))
 
 
+@pytest.mark.parametrize("spec,w,h,pf,lights,half,quarter", [
+    ("syn:C4", 160, 90, 1, 2, 0, 4096), ("syn:C4", 240, 135, 1, 2, 512, 64), ("syn:F4", 96, 54, 2, 3, 0, 4096),
+    ("ref:dodgeColorTest.obj", 200, 150, 1, 1, 0, 4096), ("syn:C4", 64, 36, 4, 2, 0, 4096), ("syn:F4", 60, 34, 3, 2, 8, 8),
+    ("syn:C4", 160, 90, 1, 16, 0, 4096), ("syn:F3", 120, 68, 1, 4, 32, 32)])
+def test_quad_walk_matches_plain_walk(spec, w, h, pf, lights, half, quarter, workdir, gpu_available):
+    """RT_TUNE_QUAD_WALK: the quarter tier's waves walk with four lanes per ray (a child box per lane,
+    DPP ranking, a leaf's triangles side by side, the quad's lexicographic minimum). Opaque (any-hit
+    shadows) and transparent (closest-hit shadows, refraction) scenes, the car's always-tested slivers,
+    pf 1, 2 and 4 (a quarter is one 16-sample pixel), pf 3 (18-sample quarters: the plain quarter tier),
+    1 to 16 lights. Frames, floats and ray counts equal the unsplit plain walk's on every launch."""
+    L = [[0, 0, 4], [1.5, 1.5, 4], [-1.5, 1.5, 4], [0, -1.5, 4]] * 4
+    p = R.RenderParams(width=w, height=h, pf=pf, max_lvl=3, lights=L[:lights])
+    with R.Scene.load(scene_path(spec, workdir), device=0) as sc:
+        sc.tune("wave_steal", 0)
+        sc.tune("chain_split", 0)
+        sc.tune("steal_half", 0)
+        sc.tune("steal_quarter", 0)
+        ref, reff, refc = sc.render(p, want_f32=True)
+        sc.tune("steal_half", half)
+        sc.tune("steal_quarter", quarter)
+        sc.tune("quad_walk", 1)
+        for i in range(4):
+            u8, f32, c = sc.render(p, want_f32=True)
+            assert [int(x) for x in c] == [int(x) for x in refc]
+            assert np.array_equal(u8, ref) and np.array_equal(f32.view(np.uint32), reff.view(np.uint32)), i
+
+
 @pytest.mark.parametrize("spec,w,h,pf,lights,half,quarter,eighth", [
     ("syn:C4", 240, 135, 1, 2, 512, 0, 0), ("syn:C4", 240, 135, 1, 4, 64, 64, 64), ("syn:F4", 96, 54, 2, 3, 512, 8, 8),
     ("ref:dodgeColorTest.obj", 200, 150, 1, 1, 512, 0, 0), ("syn:F4", 60, 34, 3, 2, 512, 8, 8),
