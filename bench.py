@@ -29,6 +29,7 @@ sys.path.insert(0, HERE)
 
 METRIC = "Mrays/s + wall-clock per frame at 1920×1080, 100k-tri OBJ"
 FLOP_PER_TEST = 37            # fp32 ops of rayIntersectTriangle's dominant path
+TEST_STAGE_FLOPS = (14, 1, 23, 5, 9)   # per stage a test reaches (rt_kernels.hip kTestStageFlops; brute-force roofline)
 FLOP_PER_NODE = 52            # BVH node visit: 2 slab tests (6 sub + 6 mul + 12 min/max each) + 2 distance culls
 FP32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector (= FP32 matrix) peak (packed FMA)
 # The same issue rate without packing (x2) or FMA (x2), which parity forbids for the triangle test:
@@ -106,7 +107,7 @@ def parse():
                     help="N=1: skip timing the shard path (tiles + un-permute) beside the frame path")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="ref_default: skip timing the drop-in's literal 'r' loop")
-    ap.add_argument("--profile-steps", type=int, default=1, help="steps re-run with HIP events for the roofline")
+    ap.add_argument("--profile-steps", type=int, default=20, help="frames re-run with HIP events for the roofline (averaged)")
     ap.add_argument("--ppm", default="", help="write the first frame to this PPM (rank 0)")
     ap.add_argument("--accel", choices=("bvh", "brute_force"), default="bvh")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c4")
@@ -481,13 +482,28 @@ def main():
     bf = None
     if args.accel == "bvh" and not args.no_bf_roofline and rank == 0:
         scene.set_accel("brute_force")
-        bst, _ = profile(1, main_run if world == 1 else Runner(1, frame_path=False))
+        brun = main_run if world == 1 else Runner(1, frame_path=False)
+        bst, _ = profile(1, brun)
+        # counted work: the stages each (query, triangle) test reached, in a separate counting pass
+        # (k_closest_hit_stages), priced per stage (rt_kernels.hip kTestStageFlops)
+        scene.reset_stats()
+        scene.set_profiling(True, count_work=True)
+        brun.render_once()
+        torch.cuda.synchronize(dev)
+        scene.set_profiling(False)
+        stages = [int(x) for x in scene.diag_read(0, len(TEST_STAGE_FLOPS))]
         scene.set_accel("bvh")
         l, ms, tests = bst[KERNEL_CLOSEST_HIT]
-        t = tests * FLOP_PER_TEST / (ms / 1e3) / 1e12
+        flops = sum(c * f for c, f in zip(stages, TEST_STAGE_FLOPS))
+        t = flops / (ms / 1e3) / 1e12
         bf = {"kernel": "k_closest_hit (brute force, --accel brute_force)", "bound": "valu",
               "achieved": round(t, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(t / FP32_PEAK_TFLOPS, 4),
               "peak_no_fma_no_pack": FP32_NOFMA_NOPACK_TFLOPS, "frac_no_fma_no_pack": round(t / FP32_NOFMA_NOPACK_TFLOPS, 4),
+              "flop_per_launch": round(flops / max(l, 1)), "tests_per_launch": round(stages[0] / max(l, 1)),
+              "stages_reached": stages, "flop_per_stage": list(TEST_STAGE_FLOPS),
+              "work_what": "counted: per (query, triangle) test, the stages of rayIntersectTriangle it reached (plane "
+                           "terms 14, division 1, in-plane coordinates and s 23, t 5, distance 9 flop; a test that "
+                           "returns early is priced at the stages it ran), from a counting pass of the same frame",
               "note": "parity forbids FMA contraction (the x86 reference has none), so the packed-FMA peak is "
                       "unreachable; the no-FMA, non-packed issue rate is the practical ceiling",
               "launches": l, "avg_launch_ms": round(ms / max(l, 1), 3), "frame_closest_hit_ms": round(ms, 3)}
@@ -541,6 +557,14 @@ def main():
                                  "profiles/r02_valu_rate.txt) / (SIMDs x launch time x 2.4 GHz); lane_utilization = "
                                  "SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU), the share of lanes active "
                                  "per issued VALU instruction"}
+        rocprof = None
+        if args.accel == "bvh":   # the same kernel's mean in the committed rocprof run (cross-check of avg_launch_ms)
+            rp, rp_src = rocprof_mean(kname, args.workload)
+            if rp and rp["mean_us"] > 0:
+                ach = flops / max(ch_launches, 1) / (rp["mean_us"] * 1e-6) / 1e12
+                rocprof = dict(rp, source=rp_src, achieved=round(ach, 3), frac=round(ach / FP32_PEAK_TFLOPS, 4),
+                               what="the same work per launch over the rocprofv3 --kernel-trace mean of the committed "
+                                    "profile (one frame in flight, launches after the first three)")
         dram = None
         if traffic and avg_s > 0:
             dram = {"achieved": round(traffic / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -614,7 +638,9 @@ def main():
                 "queries_per_launch": round(queries / max(ch_launches, 1)),
                 "launches": ch_launches,
                 "avg_launch_ms": round(avg_s * 1e3, 4),
-                "timing": "HIP events on the launch stream, batch-ordered launches of the timed entry point only",
+                "timing": f"HIP events on the launch stream, mean over {args.profile_steps} batch-ordered launches of the timed "
+                          f"entry point, one frame in flight",
+                "rocprof": rocprof,
                 "dram": dram,
                 "issue": issue,
                 "logical_bytes_per_launch": round(logical / max(ch_launches, 1)),
@@ -740,6 +766,26 @@ def strong_model(t1_ms, crit_ms, shard_ms, frame_bytes, link_gbs=(50.0, 150.0), 
                                     "pipelined_ms_per_frame": round(tp, 4), "pipelined_speedup": round(t1_ms / tp, 2)}
         out[f"n{n}"] = {"render_ms": round(render, 4), "bound": "critical path" if crit_ms >= t1_ms / n else "work / N", **res}
     return out
+
+
+def rocprof_mean(kernel: str, workload: str = "c4"):
+    """The committed rocprofv3 kernel-trace summary of `kernel` (tools/kernel_trace_summary.py over
+    tools/gpu_final.sh's rocprof run of this bench, one frame in flight): the instantiation with the
+    most launches, its mean duration after the first three launches. (dict, file) or (None, None)."""
+    import glob
+    if workload != "c4":
+        return None, None
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_kernel_trace_summary.json")), reverse=True):
+        try:
+            ks = json.load(open(f)).get("kernels", {})
+        except (OSError, ValueError):
+            continue
+        names = [n for n in ks if n == kernel or n.startswith(kernel + "<")]
+        if names:
+            n = max(names, key=lambda k: ks[k].get("launches", 0))
+            return {"instantiation": n, "launches": ks[n]["launches"], "mean_us": ks[n].get("mean_after_first_3_us", ks[n]["mean_us"])}, \
+                os.path.relpath(f, HERE)
+    return None, None
 
 
 def pmc_traffic(kernel: str, workload: str = "c4"):

@@ -146,25 +146,35 @@ __device__ __forceinline__ void sgpr_fence(const TriRec &T) {
 // kSignFirst: reject r = a / b < 0 from the signs of a and b before the division (exact: with
 // |a| > 2^-100 |b| the quotient cannot round to -0, the one negative-signed value :125 lets through),
 // so a wave whose lanes all face away from the plane skips the correctly rounded division.
-template <bool kAnyHit, bool kLex = false, bool kSignFirst = false>
+// kStages (the brute-force roofline's counting pass only): stg[k] += 1 for each stage the test reaches
+// (kTestStageFlops: 0 the plane terms, 1 the division, 2 the in-plane coordinates and s, 3 t, 4 the
+// distance), so the work a launch performed is counted, not a union path every test is assumed to take.
+constexpr int kTestStages = 5;
+constexpr int kTestStageFlops[kTestStages] = {14, 1, 23, 5, 9};
+template <bool kAnyHit, bool kLex = false, bool kSignFirst = false, bool kStages = false>
 __device__ __forceinline__ void test_triangle(const TriRec &T, int t, V3 o, V3 dir, float &best, int &bidx, V3 &bI,
-                                              bool &done) {
+                                              bool &done, unsigned *stg = nullptr) {
     if (kAnyHit && done) return;
+    if (kStages) ++stg[0];
     const V3 w0 = mk(o.x - T.t0[0], o.y - T.t0[1], o.z - T.t0[2]);
     const float b = T.n[0] * dir.x + T.n[1] * dir.y + T.n[2] * dir.z;          // :113
     const float a = -(T.n[0] * w0.x + T.n[1] * w0.y + T.n[2] * w0.z);          // :114
     if (fabsf(b) < 0.00001f) return;                                            // :115
     if (kSignFirst && (a < 0.0f) != (b < 0.0f) && fabsf(a) > fabsf(b) * 0x1p-100f) return;   // r < 0 (:125)
+    if (kStages) ++stg[1];
     const float r = a / b;                                                      // :124
     if (r < 0) return;                                                          // :125
+    if (kStages) ++stg[2];
     const V3 I = mk(o.x + dir.x * r, o.y + dir.y * r, o.z + dir.z * r);         // :130
     const V3 w = mk(I.x - T.t0[0], I.y - T.t0[1], I.z - T.t0[2]);               // :137
     const float wu = w.x * T.u[0] + w.y * T.u[1] + w.z * T.u[2];                 // :138
     const float wv = w.x * T.v[0] + w.y * T.v[1] + w.z * T.v[2];                 // :139
     const float s = (T.uv * wv - T.vv * wu) / T.D;                              // :144
     if (s < 0 || s > 1) return;                                                 // :145
+    if (kStages) ++stg[3];
     const float tt = (T.uv * wu - T.uu * wv) / T.D;                             // :148
     if (tt < 0 || (s + tt) > 1) return;                                         // :149
+    if (kStages) ++stg[4];
     const V3 e = sub(o, I);                                                     // distance, Vec3D.h:199-202
     const float dist = sqrtf(dot(e, e));
     if (dist < best || (kLex && dist == best && t < bidx)) {                  // :183
@@ -1340,6 +1350,39 @@ __global__ __launch_bounds__(kBlock) void k_closest_hit(const TriRec *__restrict
     }
 }
 
+// The brute-force closest hit's counting pass (RT_PROFILE_WORK): the same tests, one triangle per
+// iteration, with the stages each test reaches summed per kind into diag words [0, kTestStages) of
+// the work area (rt_diag_read). Results are written as k_closest_hit writes them.
+__global__ __launch_bounds__(kBlock) void k_closest_hit_stages(const TriRec *__restrict__ tris, int nt,
+                                                               const float4 *__restrict__ q_org, const float4 *__restrict__ q_dst,
+                                                               const int32_t *__restrict__ q_count, int32_t *__restrict__ hit_idx,
+                                                               float4 *__restrict__ hit_I, unsigned long long *__restrict__ diag) {
+    const int n = *q_count;
+    const int j = blockIdx.x * kBlock + threadIdx.x;
+    unsigned stg[kTestStages] = {};
+    if (j < n) {
+        const float4 qo = q_org[j], qd = q_dst[j];
+        if (as_int(qd.w) >= 0) {
+            const V3 o = mk(qo.x, qo.y, qo.z), dir = mk(qd.x - qo.x, qd.y - qo.y, qd.z - qo.z);
+            float best = FLT_MAX;
+            int bidx = -1;
+            V3 bI = mk(0, 0, 0);
+            bool done = false;
+            for (int t = 0; t < nt; ++t) test_triangle<false, false, false, true>(tris[t], t, o, dir, best, bidx, bI, done, stg);
+            hit_idx[j] = bidx;
+            hit_I[j] = make_float4(bI.x, bI.y, bI.z, 0.0f);
+        } else {
+            hit_idx[j] = -1;
+            hit_I[j] = make_float4(0, 0, 0, 0);
+        }
+    }
+    for (int k = 0; k < kTestStages; ++k) {
+        unsigned long long c = stg[k];
+        for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+        if (__lane_id() == 0 && c) atomicAdd(&diag[k], c);
+    }
+}
+
 // Shadow queries (isShadow, raytracing.cpp:241-261). With no transparent material the verdict
 // is "some triangle is hit at a distance < FLT_MAX", so lanes stop at their first such hit and
 // the wave leaves the loop once every lane has one.
@@ -1576,6 +1619,25 @@ __device__ __forceinline__ void store_chain(float4 *p, float4 v) {
     }
 }
 
+// In-lane chain records of steps < RT_LDS_RECORDS live in LDS ([step][block lane], 16 B each: 12 KB per
+// 256-lane block for 3 steps) instead of HBM: each is written and read back only by its own lane, so
+// no synchronisation is needed; deeper steps (max_lvl > 3) use w.chain_local as before.
+#ifndef RT_LDS_RECORDS
+#define RT_LDS_RECORDS 3
+#endif
+__device__ __forceinline__ float4 *lds_records() {
+    __shared__ float4 s_rec[(RT_LDS_RECORDS > 0 ? RT_LDS_RECORDS : 1) * kBvhBlock];
+    return s_rec;
+}
+__device__ __forceinline__ void put_record(const DevWork &w, int step, int sample, float4 v) {
+    if (RT_LDS_RECORDS > 0 && step < RT_LDS_RECORDS) lds_records()[step * kBvhBlock + static_cast<int>(threadIdx.x)] = v;
+    else store_chain(&w.chain_local[static_cast<int64_t>(step) * w.cap + sample], v);
+}
+__device__ __forceinline__ float4 get_record(const DevWork &w, int step, int sample) {
+    if (RT_LDS_RECORDS > 0 && step < RT_LDS_RECORDS) return lds_records()[step * kBvhBlock + static_cast<int>(threadIdx.x)];
+    return w.chain_local[static_cast<int64_t>(step) * w.cap + sample];
+}
+
 // reflection (raytracing.cpp:277-285) + addOffset (:266-271): the traced ray of level `lvl`.
 __device__ __forceinline__ void reflection_ray(V3 ray, V3 p, V3 normal, V3 &point, V3 &dest) {
     normalize(ray);
@@ -1707,7 +1769,7 @@ __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadePa
     sec.local = color;
     sec.code = sec.state | kind | (mi << 3);
     if (kInLane) {   // the caller keeps the chain (records of the steps with a child only)
-        if (sec.state == kChildTrace) store_chain(&w.chain_local[ci], make_float4(color.x, color.y, color.z, as_float(static_cast<int>(sec.code))));
+        if (sec.state == kChildTrace) put_record(w, step, sample, make_float4(color.x, color.y, color.z, as_float(static_cast<int>(sec.code))));
         return sec;
     }
     store_chain(&w.chain_local[ci], make_float4(color.x, color.y, color.z, as_float(static_cast<int>(sec.state))));
@@ -1720,7 +1782,7 @@ __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadePa
 // steps first..last-1 back to front, c_k = local_k + coef_k * c_{k+1} (fold_chain's arithmetic).
 __device__ __forceinline__ V3 fold_inlane(const DevScene &sc, const DevWork &w, int first, int last, int sample, V3 c) {
     for (int k = last - 1; k >= first; --k) {
-        const float4 L = w.chain_local[static_cast<int64_t>(k) * w.cap + sample];
+        const float4 L = get_record(w, k, sample);
         const uint32_t code = static_cast<uint32_t>(as_int(L.w));
         const DevMaterial &m = sc.mats[code >> 3];
         V3 K;
@@ -2574,6 +2636,11 @@ void launch_closest_hit(const DevScene &s, const DevWork &w, int step, int64_t c
     if (s.use_bvh) {
         if (s.bvh_width == 4) launch_ch<4>(s, w, step, capacity, stream);
         else launch_ch<2>(s, w, step, capacity, stream);
+        return;
+    }
+    if (s.work) {   // the counting pass: stages reached per test (the brute-force roofline's work)
+        hipLaunchKernelGGL(k_closest_hit_stages, dim3(grid_for(capacity)), dim3(kBlock), 0, stream, s.tris, s.nt,
+                           w.q_org[step & 1], w.q_dst[step & 1], &w.counters[step], w.hit_idx, w.hit_I, s.work + 2 * kWorkFields);
         return;
     }
     hipLaunchKernelGGL(k_closest_hit, dim3(grid_for(capacity)), dim3(kBlock), 0, stream, s.tris, s.nt,

@@ -10,3 +10,7 @@ timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method threa
 tail -2 gpurun_out/r05c_pytest.log
 timeout -k 10 600 python bench.py --steps 20 --warmup 5 --no-bf-roofline > gpurun_out/r05c_bench.json 2> gpurun_out/r05c_bench.err || { tail -30 gpurun_out/r05c_bench.err; exit 1; }
 cat gpurun_out/r05c_bench.json
+for lib in "" raytracert_amd/ab/lib_rec0.so "" raytracert_amd/ab/lib_rec0.so; do
+  env ${lib:+RTAMD_LIB=$lib} timeout -k 10 300 python -u tools/ab_frame.py c4 '[{}]' 2 40 2>&1 | grep -v amdgpu.ids | sed "s|^|[${lib:-default}] |" >> gpurun_out/r05c_ab_ldsrec.txt || exit 1
+done
+cat gpurun_out/r05c_ab_ldsrec.txt
