@@ -637,6 +637,9 @@ struct FrameCache {
     float *rec = nullptr;     // 9 floats per sub-sample: origin, dest, rgb (pinned host memory)
     size_t rec_cap = 0;
     size_t host_ray_frames = 0;   // frames whose records hold host-made rays (the host rounds differently)
+    bool host_rays = false;       // this frame's records are host-made
+    Vec3Df c[8];                  // this frame's corner rays (produceRay) and divisors
+    float divX = 0, divY = 0;
     ~FrameCache() { rt_host_free(rec); }
     bool matches(const Vec3Df &o, const Vec3Df &d) const {   // the call's ray is record `next`'s, bit for bit
         uint32_t a[6], b[6];
@@ -659,6 +662,35 @@ inline FrameCache &frame_cache() {
 
 // If (origin, dest) is the first sub-sample of the 'r' loop for the current corner rays (produceRay),
 // trace every sub-sample of that frame in one GPU call into the cache and return true.
+// The host's loop rounds differently from the device (e.g. built with FMA contraction: GCC's default
+// -ffp-contract=fast on an FMA target): make every sub-sample's ray of the cached frame with loop_ray,
+// compiled into this translation unit with the host's own flags like its loop, and trace exactly those
+// in one call (records from `next` on are then the loop's own rays and their colours).
+inline void trace_host_rays(FrameCache &fc) {
+    const size_t n = fc.n;
+    std::vector<float> o(3 * n), d(3 * n), rgb(3 * n);
+    size_t k = 0;
+    for (unsigned y = 0; y < WindowSize_Y; ++y)
+        for (unsigned x = 0; x < WindowSize_X; ++x)
+            for (int sx = 0; sx < static_cast<int>(pixelfactorX); ++sx)
+                for (int sy = 0; sy < static_cast<int>(pixelfactorY); ++sy, ++k) {
+                    Vec3Df ro, rd;
+                    loop_ray(x, y, sx, sy, fc.divX, fc.divY, fc.c, ro, rd);
+                    std::memcpy(&o[3 * k], ro.p, 12);
+                    std::memcpy(&d[3 * k], rd.p, 12);
+                }
+    const rt_params p = params(max_lvl);
+    check(rt_trace_rays(scene(), &p, o.data(), d.data(), static_cast<int32_t>(n), rgb.data(), nullptr));
+    for (k = 0; k < n; ++k) {
+        float *r = fc.rec + 9 * k;
+        std::memcpy(r, &o[3 * k], 12);
+        std::memcpy(r + 3, &d[3 * k], 12);
+        std::memcpy(r + 6, &rgb[3 * k], 12);
+    }
+    fc.host_rays = true;
+    ++fc.host_ray_frames;
+}
+
 inline bool start_frame(const Vec3Df &origin, const Vec3Df &dest) {
     if (!produceRay || WindowSize_X == 0 || WindowSize_Y == 0 || pixelfactorX == 0 || pixelfactorY == 0 || !scene())
         return false;
@@ -682,30 +714,27 @@ inline bool start_frame(const Vec3Df &origin, const Vec3Df &dest) {
     check(rt_trace_frame_samples(scene(), &p, RT_SAMPLES_RAY_RGB, fc.rec, fc.rec_cap, nullptr));
     fc.state = TraceState::now();
     fc.n = n;
+    fc.host_rays = false;
+    for (int i = 0; i < 8; ++i) fc.c[i] = c[i];
+    fc.divX = divX;
+    fc.divY = divY;
     if (fc.matches(origin, dest)) return true;   // the device's first ray is the loop's
-    // The host's loop rounds differently from the device (e.g. built with FMA contraction: GCC's default
-    // -ffp-contract=fast on an FMA target). Make the frame's rays with loop_ray, compiled into this
-    // translation unit with the host's own flags like its loop, and trace exactly those in one call; the
-    // loop's calls then hit these records (a call whose ray still differs takes the per-call path).
-    std::vector<float> o(3 * n), d(3 * n), rgb(3 * n);
-    size_t k = 0;
-    for (unsigned y = 0; y < WindowSize_Y; ++y)
-        for (unsigned x = 0; x < WindowSize_X; ++x)
-            for (int sx = 0; sx < static_cast<int>(pixelfactorX); ++sx)
-                for (int sy = 0; sy < static_cast<int>(pixelfactorY); ++sy, ++k) {
-                    Vec3Df ro, rd;
-                    loop_ray(x, y, sx, sy, divX, divY, c, ro, rd);
-                    std::memcpy(&o[3 * k], ro.p, 12);
-                    std::memcpy(&d[3 * k], rd.p, 12);
-                }
-    check(rt_trace_rays(scene(), &p, o.data(), d.data(), static_cast<int32_t>(n), rgb.data(), nullptr));
-    ++fc.host_ray_frames;
-    for (k = 0; k < n; ++k) {
-        float *r = fc.rec + 9 * k;
-        std::memcpy(r, &o[3 * k], 12);
-        std::memcpy(r + 3, &d[3 * k], 12);
-        std::memcpy(r + 6, &rgb[3 * k], 12);
-    }
+    trace_host_rays(fc);
+    return fc.matches(origin, dest);
+}
+
+// A call the cached frame did not answer, in the middle of a frame: if its ray is the host's own loop
+// ray for record `next` (the host rounds differently from the device from some sub-sample on), the
+// frame's records are remade from host rays once, and the call and the rest of the loop hit them.
+inline bool resume_frame(const Vec3Df &origin, const Vec3Df &dest) {
+    FrameCache &fc = frame_cache();
+    if (fc.host_rays || fc.next == 0 || fc.next >= fc.n || !fc.state.matches_globals()) return false;
+    const size_t spp = static_cast<size_t>(pixelfactorX) * pixelfactorY, pix = fc.next / spp, sub = fc.next % spp;
+    Vec3Df o, d;
+    loop_ray(static_cast<unsigned>(pix % WindowSize_X), static_cast<unsigned>(pix / WindowSize_X),
+             static_cast<int>(sub / pixelfactorY), static_cast<int>(sub % pixelfactorY), fc.divX, fc.divY, fc.c, o, d);
+    if (!same_bits(o, origin) || !same_bits(d, dest)) return false;
+    trace_host_rays(fc);
     return fc.matches(origin, dest);
 }
 
@@ -728,7 +757,7 @@ namespace rtamd_dropin {
 // path below stays small enough to inline into the host's loop)
 __attribute__((noinline)) inline Vec3Df perform_uncached(const Vec3Df &origin, const Vec3Df &dest) {
 #ifndef RTAMD_DROPIN_NO_FRAME_CACHE
-    if (start_frame(origin, dest)) return frame_cache().take();
+    if (start_frame(origin, dest) || resume_frame(origin, dest)) return frame_cache().take();
 #endif
     return trace(origin, dest, 0);
 }

@@ -938,9 +938,9 @@ struct QuadStack {
         return v;
     }
 };
-__device__ __forceinline__ QuadStack quad_stack(const DevScene &sc, int32_t *lds) {
+__device__ __forceinline__ QuadStack quad_stack(const DevScene &sc, int32_t *lds, int lane) {
     QuadStack st;
-    const int lane = static_cast<int>(threadIdx.x) & 63, wbase = static_cast<int>(threadIdx.x) & ~63;
+    const int wbase = static_cast<int>(threadIdx.x) & ~63;
     st.lds = lds + wbase;
     st.ovf = sc.stack_ovf;
     st.cap = 4 * sc.lds_stack;
@@ -2031,8 +2031,12 @@ template <bool kAnyHit, bool kCount>
 __device__ __forceinline__ void quad_batch(const DevScene &sc, const ShadeParams &p, const DevWork &w, const FrameGeom &g, int32_t *lds_stack,
                                            int *s_q, int *s_sh, WorkTally<kCount> &wc, WorkTally<kCount> &ws, uint8_t *out_u8,
                                            float *out_f32, int spp, int j0, int n, int nq) {
-    const int lane = __lane_id(), sl = lane >> 2, q = lane & 3, qshift = lane & ~3;
-    const QuadStack st = quad_stack(sc, lds_stack);
+    // (the lane-derived values are recomputed per part, behind an empty asm: hoisted to the kernel's
+    // start, they stayed live through the per-lane path of the other batches and spilled there)
+    int lane = __lane_id();
+    asm volatile("" : "+v"(lane));
+    const int sl = lane >> 2, q = lane & 3, qshift = lane & ~3;
+    const QuadStack st = quad_stack(sc, lds_stack, lane);
     const int j = j0 + sl;
     V3 rgb = mk(0, 0, 0);
     int px = -1;

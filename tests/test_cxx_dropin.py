@@ -223,7 +223,10 @@ def test_dropin_loop_with_fma_contraction_still_uses_frame_trace(workdir, tmp_pa
     few pixels whose rays round differently."""
     exe = _build(str(tmp_path / "dropin_fma"), ["-mfma", "-ffp-contract=fast", "-I" + os.path.join(ROOT, "include")])
     path = scene_path("ref:dodgeColorTest.obj", workdir)
-    lines = _lines([exe, "keys", path, "500", "500", str(tmp_path / "c"), "T", "T", "R"])
+    # (bounded: the per-call path would take ~150 s per frame)
+    r = subprocess.run([exe, "keys", path, "500", "500", str(tmp_path / "c"), "T", "T", "R"], check=True, capture_output=True,
+                       text=True, timeout=120)
+    lines = r.stdout.splitlines()
     fr = [l.split() for l in lines if l.startswith("frame ")]
     cache = [int(l.split()[2]) for l in lines if l.startswith("cache host_ray_frames")]
     assert float(fr[1][10]) < 5000.0, fr[1]
