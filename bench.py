@@ -212,11 +212,10 @@ def main():
             if frame_path:
                 self.fbufs = [torch.zeros(HEIGHT * WIDTH * 3, dtype=torch.uint8, device=dev)
                               for _ in range(max(2, args.inflight))]
-                # frames in flight: frame i on stream i % F (the first is the bench's stream, the others
-                # the library's rt_stream_create: each on a hardware queue of its own, so two frames never
-                # share one of the runtime's GPU_MAX_HW_QUEUES queues and run one after the other)
-                self.own_streams = [R.stream_create(local_rank) for _ in range(max(args.inflight, 1) - 1)]
-                self.fstreams = [stream] + [torch.cuda.ExternalStream(s, device=dev) for s in self.own_streams]
+                # frames in flight: frame i on stream i % F (the first is the bench's stream). (Streams on
+                # hardware queues of their own, CU-masked, made the frames overlap worse: 0.43-0.52 vs
+                # 0.35 ms per C4 frame, profiles/r05e_ab_rtstreams.txt)
+                self.fstreams = [stream] + [torch.cuda.Stream(dev) for _ in range(max(args.inflight, 1) - 1)]
                 # a new stream's first command initialises it (~6 ms of host time on this image): done
                 # here, at setup, not at the warm-up's second frame, where it left the GPU idle just
                 # before the timed frames (they then ran ~5% slow for ~25 frames)

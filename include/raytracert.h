@@ -221,12 +221,6 @@ int rt_trace_frame_samples(rt_scene *scene, const rt_params *params, int32_t lay
  * 'r' press pays only the render). samples_layout 0: the workspace only. Synchronises the device's work
  * on the scene's stream. */
 int rt_scene_reserve(rt_scene *scene, const rt_params *params, int32_t tile_w, int32_t tile_h, int32_t samples_layout);
-/* A stream (hipStream_t) on a hardware queue of its own, for hosts that keep frames in flight
- * (RT_TUNE_FRAMES_IN_FLIGHT): two ordinary streams can land on one of the runtime's shared hardware
- * queues (GPU_MAX_HW_QUEUES, 4 by default) and then run their frames one after the other. Pass it as
- * the `stream` of the render entries; destroy it with rt_stream_destroy. */
-int  rt_stream_create(int32_t device, void **stream);
-void rt_stream_destroy(void *stream);
 /* Page-locked host memory (hipHostMalloc on the scene's device's runtime), for rt_trace_frame_samples'
  * output and other large device-to-host results. */
 int  rt_host_alloc(size_t bytes, void **out);

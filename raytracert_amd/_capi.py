@@ -113,8 +113,6 @@ _SIGNATURES = {
     "rt_trace_frame_samples": ([_VP, C.POINTER(RtParams), C.c_int32, _VP, C.c_size_t, _VP], C.c_int),
     "rt_host_alloc": ([C.c_size_t, C.POINTER(_VP)], C.c_int),
     "rt_scene_reserve": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, C.c_int32], C.c_int),
-    "rt_stream_create": ([C.c_int32, C.POINTER(_VP)], C.c_int),
-    "rt_stream_destroy": ([_VP], None),
     "rt_host_free": ([_VP], None),
     "rt_render_frame_device": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, _VP, C.c_size_t, _VP, _VP], C.c_int),
     "rt_render_tiles_device": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP,

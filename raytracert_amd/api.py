@@ -496,17 +496,5 @@ def device_count() -> int:
     return n.value
 
 
-def stream_create(device: int = 0) -> int:
-    """rt_stream_create: a hipStream_t (as an int) on a hardware queue of its own, for frames in
-    flight (wrap it with torch.cuda.ExternalStream); free it with stream_destroy."""
-    s = C.c_void_p()
-    check(lib().rt_stream_create(device, C.byref(s)))
-    return int(s.value)
-
-
-def stream_destroy(stream: int) -> None:
-    lib().rt_stream_destroy(C.c_void_p(stream))
-
-
 __all__ = ["Scene", "RenderParams", "Comm", "default_corners", "write_ppm", "device_count", "ray_intersect_triangle",
-           "assemble_tiles_device", "stream_create", "stream_destroy", "RT_HOST_ONLY"]
+           "assemble_tiles_device", "RT_HOST_ONLY"]

@@ -3,7 +3,7 @@
 
 Per variant: a fresh scene, the knobs set (plus fixed ones that keep the launch trials out: wave_steal
 0, chain_split 0 unless given), 24 warm-up frames (the batch order converges), then K frames one in
-flight (back to back on one stream) and K frames two in flight (rt_stream_create streams), every
+flight (back to back on one stream) and K frames two in flight (two torch streams), every
 frame checked against the reference frame (the same knobs' first frame with all tiers off); the
 longest wave batch of the last launch (rt_batch_durations) is the critical path.
 Usage: python tools/ab_frame.py WORKLOAD '[{"knob": v, ...}, ...]' [rounds] [K]
@@ -35,7 +35,7 @@ p = R.RenderParams(width=wl["width"], height=wl["height"], pf=wl["pf"], max_lvl=
 cp = p.to_c()
 n = wl["width"] * wl["height"] * 3
 main = torch.cuda.current_stream(dev)
-side = torch.cuda.ExternalStream(R.stream_create(0), device=dev)
+side = torch.cuda.Stream(dev)
 bufs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(2)]
 ref = None
 results = {i: [] for i in range(len(variants))}

@@ -28,14 +28,11 @@ with tempfile.TemporaryDirectory() as d:
     for rnd in range(2):
         for v in variants:
             with R.Scene.load(path, device=0) as sc:
-                prio, FF, rts = False, 2, False
+                prio, FF = False, 2
                 for kv in filter(None, v.split(",")):
                     k, val = kv.split("=")
                     if k == "prio":   # frames in flight on a high- and a low-priority stream
                         prio = bool(int(val))
-                        continue
-                    if k == "rtstreams":   # the later frames on rt_stream_create streams (own hardware queues)
-                        rts = bool(int(val))
                         continue
                     if k == "F":      # frames in flight of the in-flight loop (default 2)
                         FF = int(val)
@@ -46,8 +43,6 @@ with tempfile.TemporaryDirectory() as d:
                     lo, hi = torch.cuda.Stream.priority_range()
                     streams = [torch.cuda.Stream(dev, priority=hi), torch.cuda.Stream(dev, priority=lo)]
                     main = streams[0]
-                elif rts:
-                    streams = [main] + [torch.cuda.ExternalStream(R.stream_create(0), device=dev) for _ in range(FF - 1)]
                 else:
                     streams = [main] + [torch.cuda.Stream(dev) for _ in range(FF - 1)]
                 bufs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(max(2, FF))]
