@@ -119,6 +119,7 @@ def parse():
     ap.add_argument("--orbit-step", type=float, default=0.25,
                     help="N=1: also time a moving view, each frame the view turned by this many degrees more "
                          "(scenes.orbit_corners; 0 = skip): config.orbit")
+    ap.add_argument("--no-multi-frame", action="store_true", help="skip the rt_render_frames_device leg")
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
                     help="extra launch-shape knob (Scene.tune), e.g. shadow_virtual=-1; repeatable")
     return ap.parse_args()
@@ -380,6 +381,11 @@ def main():
         # the line's value is the configured mode's (--inflight, chosen before the run); the same K
         # frames one at a time are reported beside it
 
+    # ---- several frames per call (rt_render_frames_device): one launch, one stream ----
+    multi_frame = None
+    if main_run.single and args.accel == "bvh" and not args.no_multi_frame:
+        multi_frame = multiframe_leg(scene, main_run, cparams, WIDTH, HEIGHT, args, rays_per_step, dev)
+
     # ---- a moving view: every frame a new view of an orbit (the trackball turned, then 'r') ----
     orbit = None
     if main_run.single and args.orbit_step > 0 and args.accel == "bvh":
@@ -612,6 +618,7 @@ def main():
                                          "the per-frame throughput time, one_in_flight the frame-after-frame time",
                 "one_in_flight": one_in_flight,
                 "orbit": orbit,
+                "multi_frame": multi_frame,
                 "first_frame_ms": round(cold_ms, 3) if cold_ms is not None else None,
                 "first_frame_what": "a new view's first frame (no measured batch order or launch trial: every order "
                                     "forgotten first), dispatched centre-out (RT_TUNE_COLD_ESTIMATE 2) as dynamic "
@@ -686,6 +693,39 @@ def main():
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+def multiframe_leg(scene, run, cparams, W, H, args, rays_per_frame, dev):
+    """rt_render_frames_device: K frames of the view in one chain launch (K = 2, 4), one call at a time
+    on one stream, and K = 2 with two calls in flight (RT_TUNE_FRAMES_IN_FLIGHT 2, two streams). Every
+    frame is fully rendered; ms_per_frame = wall clock / frames."""
+    import torch
+    K_MAX = 4
+    bufs = [torch.zeros(H * W * 3, dtype=torch.uint8, device=dev) for _ in range(2 * K_MAX)]
+    out = {"what": "K frames of the view per rt_render_frames_device call (one chain launch whose wave tasks cycle "
+                   "over the frames), calls back to back; every frame fully rendered"}
+    for K, fif in ((2, 1), (4, 1), (2, 2)):
+        scene.tune("frames_in_flight", fif)
+        calls = max(args.steps // K, 2)
+
+        def call(i):
+            st = run.fstreams[i % fif] if fif <= len(run.fstreams) else run.fstreams[0]
+            base = (i % 2) * K
+            scene.render_frames_device([cparams] * K, TILE, TILE, [b.data_ptr() for b in bufs[base:base + K]], bufs[0].numel(),
+                                       st.cuda_stream)
+        for i in range(max(args.warmup, 2) * fif):
+            call(i)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(calls):
+            call(i)
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        frames = calls * K
+        out[f"k{K}_inflight{fif}"] = {"frames": frames, "ms_per_frame": round(el / frames * 1e3, 4),
+                                      "value": round(rays_per_frame * frames / el / 1e6, 4)}
+    scene.tune("frames_in_flight", 1)
+    return out
 
 
 def orbit_leg(scene, run, W, H, PF, MAX_LVL, LIGHTS, flags, args, inflight, obj, dev):

@@ -20,6 +20,7 @@
  *                         + RGBValue clamp :24-42 + Image::writeImage quantisation :102-128)
  *   rt_render_tiles_device  same loop, interleaved tile shard into a device buffer (multi-GPU)
  *   rt_render_frame_device  same loop, the whole frame into a device buffer (single GPU)
+ *   rt_render_frames_device  the loop for several views in one launch (consecutive 'r' presses)
  *   rt_render_frames_sharded  the same loop over N GPUs     (nothing in the reference: SURVEY.md §8e)
  *   rt_comm_*             RCCL communicator for it          (one process or host thread per GPU)
  *   rt_default_corners    produceRay for the 4 corners      main.cpp:300-325,355-358 (+ reshape :288-296)
@@ -230,6 +231,18 @@ void rt_host_free(void *ptr);
  * The single-GPU form of the shard + gather path (no un-permute needed). */
 int rt_render_frame_device(rt_scene *scene, const rt_params *params, int32_t tile_w, int32_t tile_h, void *d_out_u8,
                            size_t out_capacity, void *stream, uint64_t counts[3]);
+/* Several frames of one frame geometry, each its own view: params[f] (f < n_frames) may differ from
+ * params[0] in their corner rays only (the trackball turned between 'r' presses, main.cpp:355-358), and
+ * frame f goes row-major into the DEVICE buffer d_out_u8[f] (each out_capacity bytes). One chain launch
+ * renders all of them when the frame is one batch of the four-wide tree (C4, C5): its wave tasks cycle
+ * over the frames, so the frames' longest batches start side by side and the short ones of each fill
+ * the slots the others' tails free, on one stream and one hardware queue (the overlap frames in flight
+ * on two streams get, without depending on the runtime placing those streams on different hardware
+ * queues). Otherwise the frames render one after another. Bytes equal the frames rendered one at a
+ * time. counts: the sum over the frames. Stream semantics as rt_render_tiles_device. */
+#define RT_MAX_FRAMES_PER_CALL 4
+int rt_render_frames_device(rt_scene *scene, const rt_params *params, int32_t n_frames, int32_t tile_w, int32_t tile_h,
+                            void *const *d_out_u8, size_t out_capacity, void *stream, uint64_t counts[3]);
 int rt_render_tiles_device(rt_scene *scene, const rt_params *params, int32_t tile_w, int32_t tile_h,
                            int32_t frames, int32_t first, int32_t stride, void *d_out_u8, size_t out_capacity,
                            void *stream, int32_t *n_tiles_out, uint64_t counts[3]);

@@ -52,6 +52,7 @@ TUNE_ADOPT_ORDER = 32
 TUNE_INFLIGHT_DYNAMIC = 33
 TUNE_INFLIGHT_STREAMS = 34
 TUNE_QUAD_WALK = 35
+MAX_FRAMES_PER_CALL = 4   # RT_MAX_FRAMES_PER_CALL
 BVH_INFO_FIELDS = 7
 STOCHASTIC = 1 << 8
 DEFAULT_SEED = 0x5EED
@@ -113,6 +114,8 @@ _SIGNATURES = {
     "rt_trace_frame_samples": ([_VP, C.POINTER(RtParams), C.c_int32, _VP, C.c_size_t, _VP], C.c_int),
     "rt_host_alloc": ([C.c_size_t, C.POINTER(_VP)], C.c_int),
     "rt_scene_reserve": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, C.c_int32], C.c_int),
+    "rt_render_frames_device": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, C.c_int32, C.POINTER(_VP), C.c_size_t, _VP, _VP],
+                                C.c_int),
     "rt_host_free": ([_VP], None),
     "rt_render_frame_device": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, _VP, C.c_size_t, _VP, _VP], C.c_int),
     "rt_render_tiles_device": ([_VP, C.POINTER(RtParams), C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _VP,

@@ -238,6 +238,23 @@ class Scene:
         check(lib().rt_trace_frame_samples(self._h, C.byref(p), layout, _ptr(rec), rec.size, _ptr(counts)))
         return rec, counts
 
+    def render_frames_device(self, params: Sequence[RenderParams | RtParams], tile_w: int, tile_h: int, out_ptrs: Sequence[int],
+                             out_capacity: int, stream_ptr: int | None = None, want_counts: bool = False):
+        """rt_render_frames_device: len(params) views of one frame geometry (params differ in corners only),
+        view f row-major into the device buffer out_ptrs[f], in one chain launch where possible."""
+        n = len(params)
+        arr = (RtParams * n)()
+        keep = []
+        for i, q in enumerate(params):
+            c = q.to_c() if isinstance(q, RenderParams) else q
+            keep.append(c)
+            arr[i] = c
+        outs = (C.c_void_p * n)(*[C.c_void_p(x) for x in out_ptrs])
+        counts = np.zeros(3, np.uint64) if want_counts else None
+        check(lib().rt_render_frames_device(self._h, arr, n, tile_w, tile_h, outs, out_capacity,
+                                            C.c_void_p(stream_ptr) if stream_ptr else None, _ptr(counts)))
+        return counts
+
     def reserve(self, params: RenderParams | RtParams, tile_w: int = 16, tile_h: int = 16, samples_layout: int = 0):
         """rt_scene_reserve: allocate what a frame of params needs (workspaces, sample staging) now,
         so its first render allocates nothing."""

@@ -35,6 +35,18 @@ struct FrameGeom {
     UDiv div_spp, div_tpx, div_tiles, div_tx, div_tw, div_pfy;
 };
 
+// A multi-frame chain launch (rt_render_frames_device): frames 0..count-1 of one frame geometry that
+// differ only in their corner rays (views) and outputs. The launch's wave tasks cycle over the frames
+// (task t: frame t % count, the frame's own task t / count), so the frames' longest batches start side
+// by side and their short ones fill the slots the others' tails free, in one launch on one queue.
+constexpr int kMaxFramesPerLaunch = 4;
+struct FrameSet {
+    int32_t count;                                  // 1: a single frame (the FrameGeom's corners and outputs)
+    float corners[kMaxFramesPerLaunch][8][3];
+    uint8_t *out_u8[kMaxFramesPerLaunch];
+    float *out_f32[kMaxFramesPerLaunch];
+};
+
 struct ShadeParams {
     int32_t max_lvl;
     uint32_t flags;
@@ -154,9 +166,10 @@ int chain_blocks_per_cu();   // blocks of the chain kernels resident per CU (4 S
 int bvh_block_threads();     // threads per block of the BVH and chain kernels (RT_BVH_BLOCK)
 int chain_spb(int fuse_spp);                            // samples per wave batch of a fused launch
 int64_t chain_batches(int64_t capacity, int fuse_spp);  // wave batches of a launch over `capacity` samples
+// fs (fused launches only, may be null): a multi-frame launch over fs->count views of g (FrameSet).
 void launch_chain(const DevScene &s, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
                   hipStream_t stream, bool ordered = false, uint8_t *out_u8 = nullptr, float *out_f32 = nullptr,
-                  int fuse_spp = 0, const FrameGeom *g = nullptr);
+                  int fuse_spp = 0, const FrameGeom *g = nullptr, const FrameSet *fs = nullptr);
 void launch_fold_rays(const DevWork &w, int32_t n, float *rgb, hipStream_t stream);
 // The chain kernels read their arguments through a struct view of the kernel-argument segment
 // (RT_OPAQUE_ARGS): a probe kernel with k_chain's parameter list checks that view against the bytes

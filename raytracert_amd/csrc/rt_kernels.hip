@@ -1471,7 +1471,9 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
 // Sample s of a batch (main.cpp:355-395 for one sub-sample): its pixel, its output index px (the
 // tile-major shard slot or the row-major index in the clip rectangle) and its primary ray; false for
 // samples outside the frame or the clip rectangle (origin and dest then (0,0,0)).
-__device__ __forceinline__ bool primary_sample(const FrameGeom &g, int64_t s, V3 &origin, V3 &dest, int64_t &px, int &sub) {
+// cs: the corner rays (g.corners, or a multi-frame launch's frame's: primary_sample_view)
+__device__ __forceinline__ bool primary_sample_view(const FrameGeom &g, const float (*cs)[3], int64_t s, V3 &origin, V3 &dest,
+                                                    int64_t &px, int &sub) {
     const int spp = g.pfx * g.pfy;
     const int64_t pix = udiv(static_cast<uint32_t>(s), g.div_spp);
     sub = static_cast<int>(s - pix * spp);
@@ -1496,14 +1498,14 @@ __device__ __forceinline__ bool primary_sample(const FrameGeom &g, int64_t s, V3
         }
         const float xscale = 1.0f - (static_cast<float>(static_cast<unsigned>(x)) * static_cast<float>(static_cast<unsigned>(g.pfx)) + fx) / g.divX;  // :380
         const float yscale = 1.0f - (static_cast<float>(static_cast<unsigned>(y)) * static_cast<float>(static_cast<unsigned>(g.pfy)) + fy) / g.divY;  // :381
-        const V3 o00 = mk(g.corners[0][0], g.corners[0][1], g.corners[0][2]);
-        const V3 d00 = mk(g.corners[1][0], g.corners[1][1], g.corners[1][2]);
-        const V3 o01 = mk(g.corners[2][0], g.corners[2][1], g.corners[2][2]);
-        const V3 d01 = mk(g.corners[3][0], g.corners[3][1], g.corners[3][2]);
-        const V3 o10 = mk(g.corners[4][0], g.corners[4][1], g.corners[4][2]);
-        const V3 d10 = mk(g.corners[5][0], g.corners[5][1], g.corners[5][2]);
-        const V3 o11 = mk(g.corners[6][0], g.corners[6][1], g.corners[6][2]);
-        const V3 d11 = mk(g.corners[7][0], g.corners[7][1], g.corners[7][2]);
+        const V3 o00 = mk(cs[0][0], cs[0][1], cs[0][2]);
+        const V3 d00 = mk(cs[1][0], cs[1][1], cs[1][2]);
+        const V3 o01 = mk(cs[2][0], cs[2][1], cs[2][2]);
+        const V3 d01 = mk(cs[3][0], cs[3][1], cs[3][2]);
+        const V3 o10 = mk(cs[4][0], cs[4][1], cs[4][2]);
+        const V3 d10 = mk(cs[5][0], cs[5][1], cs[5][2]);
+        const V3 o11 = mk(cs[6][0], cs[6][1], cs[6][2]);
+        const V3 d11 = mk(cs[7][0], cs[7][1], cs[7][2]);
         const float ix = 1 - xscale, iy = 1 - yscale;
         origin = add(scale(add(scale(o00, xscale), scale(o10, ix)), yscale),
                      scale(add(scale(o01, xscale), scale(o11, ix)), iy));                     // :383-384
@@ -1511,6 +1513,9 @@ __device__ __forceinline__ bool primary_sample(const FrameGeom &g, int64_t s, V3
                    scale(add(scale(d01, xscale), scale(d11, ix)), iy));                       // :385-386
     }
     return valid;
+}
+__device__ __forceinline__ bool primary_sample(const FrameGeom &g, int64_t s, V3 &origin, V3 &dest, int64_t &px, int &sub) {
+    return primary_sample_view(g, g.corners, s, origin, dest, px, sub);
 }
 
 // Also resets the batch's queue counters and work-queue slots (counter 0 = the queue's size), so
@@ -2028,7 +2033,8 @@ __device__ __forceinline__ Secondary chain_step_quad(const DevScene &sc, const S
 // then the part's whole pixels are summed in sub-sample order across quads (k_frame's arithmetic) and
 // written by the pixel's first quad's lane 0. n <= kQuadSamples (the host enables the tier only then).
 template <bool kAnyHit, bool kCount>
-__device__ __forceinline__ void quad_batch(const DevScene &sc, const ShadeParams &p, const DevWork &w, const FrameGeom &g, int32_t *lds_stack,
+__device__ __forceinline__ void quad_batch(const DevScene &sc, const ShadeParams &p, const DevWork &w, const FrameGeom &g,
+                                           const float (*cs)[3], int32_t *lds_stack,
                                            int *s_q, int *s_sh, WorkTally<kCount> &wc, WorkTally<kCount> &ws, uint8_t *out_u8,
                                            float *out_f32, int spp, int j0, int n, int nq) {
     // (the lane-derived values are recomputed per part, behind an empty asm: hoisted to the kernel's
@@ -2044,7 +2050,7 @@ __device__ __forceinline__ void quad_batch(const DevScene &sc, const ShadeParams
         V3 org, dst;
         int64_t pxi = 0;
         int sub = 0;
-        if (!primary_sample(g, j, org, dst, pxi, sub)) {
+        if (!primary_sample_view(g, cs, j, org, dst, pxi, sub)) {
             if (g.out_mode == 0 && out_u8 && sub == 0 && q == 0) { out_u8[3 * pxi] = 0; out_u8[3 * pxi + 1] = 0; out_u8[3 * pxi + 2] = 0; }
         } else {
             px = g.out_mode == 2 ? static_cast<int>(pxi) * spp + sub : static_cast<int>(pxi);
@@ -2105,6 +2111,7 @@ struct ChainKernargs {
     int fuse_spp, spb, nbatch;
     FrameGeom g;
     int split, split8;
+    FrameSet fs;
 };
 
 // Bit k set: argument k of k_chain is not where ChainKernargs places it. The probe launch fills each
@@ -2114,7 +2121,7 @@ struct ChainKernargs {
 // (distinct sentinels). Bit 31 marks that the probe ran. (Taking the formals' addresses instead made
 // the compiler copy them into 736 B of scratch per lane.)
 constexpr uint32_t kKargTagScene = 0xA0000000u, kKargTagShade = 0xB0000000u, kKargTagWork = 0xC0000000u,
-                   kKargTagGeom = 0xD0000000u;
+                   kKargTagGeom = 0xD0000000u, kKargTagFrames = 0xE0000000u;
 template <typename T>
 __device__ __forceinline__ uint32_t karg_words_differ(const __attribute__((address_space(4))) T *m, uint32_t tag) {
     const __attribute__((address_space(4))) uint32_t *u = (const __attribute__((address_space(4))) uint32_t *)m;
@@ -2140,12 +2147,13 @@ __device__ __forceinline__ uint32_t chain_kernarg_mismatch(int first, int ordere
     bad |= karg_words_differ(&ka->g, kKargTagGeom) << 10;
     bad |= static_cast<uint32_t>(ka->split != split) << 11;
     bad |= static_cast<uint32_t>(ka->split8 != split8) << 12;
+    bad |= karg_words_differ(&ka->fs, kKargTagFrames) << 13;
     return bad;
 }
-template <int W, bool kAnyHit, bool kCount, bool kInLane = false, bool kSteal = false, bool kQuad = false>
+template <int W, bool kAnyHit, bool kCount, bool kInLane = false, bool kSteal = false, bool kQuad = false, bool kMulti = false>
 __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kSteal ? RT_STEAL_WPE : RT_CHAIN_WPE))) void k_chain(
     const DevScene sc, const ShadeParams p, DevWork w, int first, int ordered, uint8_t *__restrict__ out_u8,
-    float *__restrict__ out_f32, int fuse_spp, int spb, int nbatch, const FrameGeom g, int split, int split8) {
+    float *__restrict__ out_f32, int fuse_spp, int spb, int nbatch, const FrameGeom g, int split, int split8, const FrameSet fs) {
     extern __shared__ int32_t lds_stack[];
     __shared__ int s_q[kChainSteps], s_sh[kChainSteps];
 #if RT_LDS_PARK
@@ -2189,7 +2197,10 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
     // time from per-XCD counters in the (self-reset) counter buffer by a resident grid, so no wave
     // slot waits for the other waves of its block to retire; in batch order when ordered
     const bool dyn = kInLane && sc.chain_split == 4;
-    drive_queries((nbatch + extra) * kWave, dyn ? 4 : (sc.chain_split & 3), dyn ? &w.counters[kWaveQueueSlot] : w.wq + (2 * first) * kWqSlot,
+    // a multi-frame launch (FrameSet): task t is frame t % nfr's task t / nfr
+    // (its own instantiation, kMulti: the frame bookkeeping moved the default kernel's spill 32 -> 44 B)
+    const int nfr = (kInLane && kMulti) ? max(1, fs.count) : 1;
+    drive_queries((nbatch + extra) * kWave * nfr, dyn ? 4 : (sc.chain_split & 3), dyn ? &w.counters[kWaveQueueSlot] : w.wq + (2 * first) * kWqSlot,
                   [&](int j0, int vend) {
 #if RT_OPAQUE_ARGS
         // the frame geometry, shading parameters, scene and workspace are read from the kernel
@@ -2216,7 +2227,23 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         const DevScene &scb = sc;
         const DevWork &wb = w;
 #endif
-        const int vb = j0 >> 6;   // this wave's virtual batch (wave-uniform for the orderable distributions)
+        const int vball = j0 >> 6;   // this wave's virtual batch (wave-uniform for the orderable distributions)
+        const int fr = nfr > 1 ? vball % nfr : 0, vb = nfr > 1 ? vball / nfr : vball;   // (its frame, its batch in it)
+        // the frame's outputs, read where they are written (held from the batch's start, they stayed live
+        // through the chain and spilled), and its corner rays
+#if RT_OPAQUE_ARGS
+        auto frame_out = [&](auto which) {
+            KargPtr kb = (KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
+            asm volatile("" : "+s"(kb));
+            return which(nfr > 1, kb->fs.out_u8[fr], kb->fs.out_f32[fr], kb->out_u8, kb->out_f32);
+        };
+        const float(*const fcs)[3] = (const float(*)[3]) & ka->fs.corners[fr][0];
+#else
+        auto frame_out = [&](auto which) { return which(nfr > 1, fs.out_u8[fr], fs.out_f32[fr], out_u8, out_f32); };
+        const float(*const fcs)[3] = fs.corners[fr];
+#endif
+        auto o8f = [&]() { return frame_out([](bool m, uint8_t *a, float *, uint8_t *c, float *) { return m ? a : c; }); };
+        auto of32f = [&]() { return frame_out([](bool m, uint8_t *, float *b, uint8_t *, float *d) { return m ? b : d; }); };
         // split tiers of the order: 8 parts, then 4, then 2; part = which part of batch order[ob]
         int ob = vb - (ordered ? extra : 0), nparts = 1, part = 0;
         if (ordered) {
@@ -2230,7 +2257,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
             else __builtin_amdgcn_s_setprio(0);
         }
         const int plen = ((ppb + nparts - 1) / nparts) * spp;   // whole pixels per part
-        const bool wave_on = (vb << 6) < vend;
+        const bool wave_on = (vball << 6) < vend;
         const int pb = (ordered && wave_on) ? wb.batch_order[ob] : vb;
         const int lane_off = nparts > 1 ? part * plen + lane : (j0 & (kWave - 1));
         // (unordered, the XCD-segment distributions hand out unaligned ranges: the lane's own bound)
@@ -2247,8 +2274,8 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         const bool quad = kQuad && kInLane && !kSteal && W == 4 && nparts == 4 && scb.quad_walk && plen <= kQuadSamples;
         if (quad) {
             if (wave_on)
-                quad_batch<kAnyHit, kCount>(scb, pl, wb, gl, lds_stack, s_q, s_sh, wc, ws, out_u8, out_f32, fuse_spp,
-                                            pb * spb + part * plen, min(plen, spb - part * plen), nq);
+                quad_batch<kAnyHit, kCount>(scb, pl, wb, gl, nfr > 1 ? fcs : gl.corners, lds_stack, s_q, s_sh, wc, ws, o8f(), of32f(),
+                                            fuse_spp, pb * spb + part * plen, min(plen, spb - part * plen), nq);
         } else {
         const int roles = (kInLane && !kSteal && nparts > 1 && scb.shadow_helpers && (pl.flags & RT_SHADOWS))
                               ? max(1, min(kWave / plen, pl.n_lights)) : 1;
@@ -2260,8 +2287,9 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         if (kInLane) {   // sample j: its primary ray, as k_gen_primary makes it
             int64_t pxi = 0;
             int sub = 0;
-            if (own && !primary_sample(gl, j, org, dst, pxi, sub)) {
-                if (gl.out_mode == 0 && out_u8 && sub == 0) { out_u8[3 * pxi] = 0; out_u8[3 * pxi + 1] = 0; out_u8[3 * pxi + 2] = 0; }
+            if (own && !(nfr > 1 ? primary_sample_view(gl, fcs, j, org, dst, pxi, sub) : primary_sample(gl, j, org, dst, pxi, sub))) {
+                uint8_t *const o8 = o8f();
+                if (gl.out_mode == 0 && o8 && sub == 0) { o8[3 * pxi] = 0; o8[3 * pxi + 1] = 0; o8[3 * pxi + 2] = 0; }
                 own = false;
             }
             if (roles > 1) {   // a helper follows its owner's sample (all lanes are still here)
@@ -2271,7 +2299,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
             if (!own || (role == 0 && !lane_on)) return;
             if (role == 0) px = gl.out_mode == 2 ? static_cast<int>(pxi) * fuse_spp + sub : static_cast<int>(pxi);
             if (gl.out_mode == 2 && gl.sample_stride == 9 && role == 0) {   // the record's ray (RT_SAMPLES_RAY_RGB)
-                float *r = out_f32 + 9 * static_cast<int64_t>(px);
+                float *r = of32f() + 9 * static_cast<int64_t>(px);
                 r[0] = org.x; r[1] = org.y; r[2] = org.z; r[3] = dst.x; r[4] = dst.y; r[5] = dst.z;
             }
             lvl = 0;
@@ -2308,7 +2336,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         }();
         if (kInLane && gl.out_mode == 2) {   // every sub-sample's own colour (rt_trace_frame_samples)
             if (px >= 0) {
-                float *o = out_f32 + static_cast<int64_t>(gl.sample_stride) * px + (gl.sample_stride - 3);
+                float *o = of32f() + static_cast<int64_t>(gl.sample_stride) * px + (gl.sample_stride - 3);
                 o[0] = rgb.x; o[1] = rgb.y; o[2] = rgb.z;
             }
         } else if (kInLane) {   // k_frame's arithmetic: a pixel's fuse_spp sub-samples sit in adjacent lanes
@@ -2317,7 +2345,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
                 acc = add(acc, mk(__shfl(rgb.x, pix_lane + sub), __shfl(rgb.y, pix_lane + sub), __shfl(rgb.z, pix_lane + sub)));
             const float div = static_cast<float>(fuse_spp);
             acc = mk(acc.x / div, acc.y / div, acc.z / div);   // operator/, Vec3D.h:36-38
-            if (lane == pix_lane && px >= 0) store_pixel(acc, 3 * static_cast<int64_t>(px), out_u8, out_f32);
+            if (lane == pix_lane && px >= 0) store_pixel(acc, 3 * static_cast<int64_t>(px), o8f(), of32f());
         }
         }
         // the batch's lifetime (a split batch: its parts' lifetimes, the last to finish stored), with
@@ -2711,14 +2739,15 @@ int64_t chain_batches(int64_t capacity, int fuse_spp) {
 
 // k_chain's instantiations by width, any-hit shadows, work counting, fused frame and stealing
 typedef void (*ChainKernel)(const DevScene, const ShadeParams, DevWork, int, int, uint8_t *, float *, int, int, int,
-                            const FrameGeom, int, int);
+                            const FrameGeom, int, int, const FrameSet);
 // The layout probe: a kernel with exactly k_chain's parameter list (both are ChainKernel, checked
 // below), so its kernel-argument segment is laid out as every k_chain instantiation's. It runs
 // chain_kernarg_mismatch once. (Inside k_chain, even behind an early return, the check moved the
 // register allocation: spill 24 -> 36 B per lane.)
 __global__ __launch_bounds__(64) void k_chain_kernarg_probe(const DevScene sc, const ShadeParams p, DevWork w, int first, int ordered,
                                                            uint8_t *__restrict__ out_u8, float *__restrict__ out_f32, int fuse_spp,
-                                                           int spb, int nbatch, const FrameGeom g, int split, int split8) {
+                                                           int spb, int nbatch, const FrameGeom g, int split, int split8,
+                                                           const FrameSet fs) {
     if (blockIdx.x == 0 && threadIdx.x == 0)
         *reinterpret_cast<uint32_t *>(out_u8) = chain_kernarg_mismatch(first, ordered, out_u8, out_f32, fuse_spp, spb, nbatch, split,
                                                                        split8);
@@ -2726,10 +2755,10 @@ __global__ __launch_bounds__(64) void k_chain_kernarg_probe(const DevScene sc, c
 static_assert(std::is_same<decltype(&k_chain_kernarg_probe), ChainKernel>::value, "the probe must have k_chain's parameters");
 static_assert(std::is_same<decltype(&k_chain<4, true, false, true, false>), ChainKernel>::value, "k_chain's parameters changed");
 
-template <int W, bool kInLane, bool kSteal, bool kQuad = false>
+template <int W, bool kInLane, bool kSteal, bool kQuad = false, bool kMulti = false>
 ChainKernel chain_kernel(bool anyhit, bool count) {
-    return anyhit ? (count ? k_chain<W, true, true, kInLane, kSteal, kQuad> : k_chain<W, true, false, kInLane, kSteal, kQuad>)
-                  : (count ? k_chain<W, false, true, kInLane, kSteal, kQuad> : k_chain<W, false, false, kInLane, kSteal, kQuad>);
+    return anyhit ? (count ? k_chain<W, true, true, kInLane, kSteal, kQuad, kMulti> : k_chain<W, true, false, kInLane, kSteal, kQuad, kMulti>)
+                  : (count ? k_chain<W, false, true, kInLane, kSteal, kQuad, kMulti> : k_chain<W, false, false, kInLane, kSteal, kQuad, kMulti>);
 }
 
 // k_chain_kernarg_probe once (one wave, tagged structures, sentinel scalars): *bad = its word unless
@@ -2751,13 +2780,15 @@ hipError_t probe_chain_kernargs(hipStream_t stream, uint32_t *bad, int *which) {
     ShadeParams sp;
     DevWork w;
     FrameGeom g;
+    FrameSet fs;
     tagged(sc, kKargTagScene);
     tagged(sp, kKargTagShade);
     tagged(w, kKargTagWork);
     tagged(g, kKargTagGeom);
+    tagged(fs, kKargTagFrames);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_chain_kernarg_probe, dim3(1), dim3(64), 0, stream, sc, sp, w, 0x11, -1, reinterpret_cast<uint8_t *>(d),
-                           reinterpret_cast<float *>(static_cast<uintptr_t>(0x1234560)), 0x21, 0x31, 0x41, g, 0x51, 0x61);
+                           reinterpret_cast<float *>(static_cast<uintptr_t>(0x1234560)), 0x21, 0x31, 0x41, g, 0x51, 0x61, fs);
         e = hipGetLastError();
     }
     uint32_t h = 0;
@@ -2770,7 +2801,8 @@ hipError_t probe_chain_kernargs(hipStream_t stream, uint32_t *bad, int *which) {
 }
 
 void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, int first, int64_t capacity,
-                  hipStream_t stream, bool ordered, uint8_t *out_u8, float *out_f32, int fuse_spp, const FrameGeom *g) {
+                  hipStream_t stream, bool ordered, uint8_t *out_u8, float *out_f32, int fuse_spp, const FrameGeom *g,
+                  const FrameSet *fs) {
     if (capacity <= 0) return;
     const bool wide = s0.bvh_width == 4;
     const DevScene s = for_width(s0, wide ? 4 : 2);
@@ -2798,7 +2830,10 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
     // the quarter tier as quad walks (RT_TUNE_QUAD_WALK) when a quarter holds at most 16 samples
     const int ppb_f = fused ? spb / fuse_spp : 0;
     const bool quad = wide && fused && !steal && s.quad_walk && s4 > 0 && ((ppb_f + 3) / 4) * fuse_spp <= kQuadSamples;
-    ChainKernel k = steal  ? chain_kernel<4, true, true>(anyhit, count)
+    const bool multi = fused && wide && !quad && fs && fs->count > 1;   // (host: 4-wide fused launches only)
+    ChainKernel k = (steal && multi) ? chain_kernel<4, true, true, false, true>(anyhit, count)
+                  : steal  ? chain_kernel<4, true, true>(anyhit, count)
+                  : multi  ? chain_kernel<4, true, false, false, true>(anyhit, count)
                   : quad   ? chain_kernel<4, true, false, true>(anyhit, count)
                   : fused  ? (wide ? chain_kernel<4, true, false>(anyhit, count) : chain_kernel<2, true, false>(anyhit, count))
                            : (wide ? chain_kernel<4, false, false>(anyhit, count) : chain_kernel<2, false, false>(anyhit, count));
@@ -2806,9 +2841,12 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
     const FrameGeom geom = g ? with_divisors(*g) : FrameGeom{};
     // distribution 4 (dynamic wave tasks): a resident grid, each wave takes tasks until none remain
     const int grid_cap = (fused && s.chain_split == 4) ? std::max(1, std::min(s.bvh_grid, s.resident_grid)) : s.bvh_grid;
-    hipLaunchKernelGGL(k, dim3(grid_bvh((nbatch + 7 * s8 + 3 * s4 + s2) * kWave, grid_cap)), dim3(kBvhBlock), bvh_lds(s), stream, s,
-                       p, w, first, ordered ? 1 : 0, out_u8, out_f32, fused ? fuse_spp : 0, spb, static_cast<int>(nbatch),
-                       geom, split, s8);
+    FrameSet frames{};
+    frames.count = 1;
+    if (multi) frames = *fs;
+    hipLaunchKernelGGL(k, dim3(grid_bvh((nbatch + 7 * s8 + 3 * s4 + s2) * kWave * frames.count, grid_cap)), dim3(kBvhBlock), bvh_lds(s),
+                       stream, s, p, w, first, ordered ? 1 : 0, out_u8, out_f32, fused ? fuse_spp : 0, spb, static_cast<int>(nbatch),
+                       geom, split, s8, frames);
 }
 
 void launch_estimate(const DevScene &s0, const ShadeParams &p, const FrameGeom &g, int fuse_spp, int64_t capacity,
