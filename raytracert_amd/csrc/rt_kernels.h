@@ -164,6 +164,7 @@ void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *
 // ordered: dispatch the wave batches by w.batch_order (the previous launch's measured durations).
 int chain_blocks_per_cu();   // blocks of the chain kernels resident per CU (4 SIMDs x waves per EU x 64 / block)
 int bvh_block_threads();     // threads per block of the BVH and chain kernels (RT_BVH_BLOCK)
+int chain_lds_record_steps();   // fused chain launches keep the records of steps below this in LDS (RT_LDS_RECORDS)
 int chain_spb(int fuse_spp);                            // samples per wave batch of a fused launch
 int64_t chain_batches(int64_t capacity, int fuse_spp);  // wave batches of a launch over `capacity` samples
 // fs (fused launches only, may be null): a multi-frame launch over fs->count views of g (FrameSet).

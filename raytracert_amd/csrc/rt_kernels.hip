@@ -2866,6 +2866,7 @@ void launch_estimate(const DevScene &s0, const ShadeParams &p, const FrameGeom &
 }
 
 int chain_blocks_per_cu() { return 4 * RT_CHAIN_WPE * kWave / kBvhBlock; }
+int chain_lds_record_steps() { return RT_LDS_RECORDS; }
 int bvh_block_threads() { return kBvhBlock; }
 
 void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *out_f32, hipStream_t stream) {

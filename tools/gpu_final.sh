@@ -21,6 +21,6 @@ timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/ben
 cat gpurun_out/bench_$TAG.json
 # rocprof of the timed entry point: 50 ordered frames dilute the first (unordered) launches; the
 # trace summary also gives the mean over launches after the first 3
-(cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof/$TAG" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 500 --warmup 30 --inflight 1 --no-cpu --no-cold --no-path-compare --no-bf-roofline > "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log" 2>&1) || { echo "rocprof failed"; tail -20 gpurun_out/prof_$TAG.log; exit 1; }
+(cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof/$TAG" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 500 --warmup 30 --inflight 1 --no-cpu --no-cold --no-path-compare --no-bf-roofline --orbit-step 0 --no-multi-frame --profile-steps 1 > "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log" 2>&1) || { echo "rocprof failed"; tail -20 gpurun_out/prof_$TAG.log; exit 1; }
 python3 tools/kernel_trace_summary.py gpurun_out/prof/$TAG 3 > gpurun_out/${TAG}_kernel_trace_summary.json || exit 1
 [ -n "$NO_WORKLOADS" ] || bash tools/gpu_workloads.sh $TAG || exit 1
