@@ -118,6 +118,13 @@ extern "C" {
                                     path) finish sooner; a part then holds at most 16 samples of whole pixels
                                     (pf 1, 2, 4; otherwise the plain quarter tier). 0 (default): off.
                                     Placement only */
+#define RT_TUNE_MOTION_ORDER 36   /* 1 (default): a fused frame whose corner rays differ from the previous launch of its
+                                    pipeline over the same batches (a moving view: the trackball turned between
+                                    'r' presses) re-sorts the batch order after every launch, from the durations
+                                    dilated over the screen (each batch takes the longest duration within the
+                                    3 x 3 cells of 8 x 8 pixels around it), so a long batch that moved by a few
+                                    pixels is still near the head; 0: the static schedule (every
+                                    RT_TUNE_ORDER_EVERY launches, undilated). Placement only */
 #define RT_TUNE_TOP_NODES 13     /* retired in r03 (0-85 accepted, no effect): an LDS copy of the four-wide
                                     tree's top levels; with float node rows loaded from global memory it
                                     measured slower (flat loads, 64-bit addresses) */
@@ -169,7 +176,7 @@ int rt_batch_durations(rt_scene *scene, uint32_t *ticks, int64_t capacity, int64
  * in carving order, (offset, bytes): q_org[0], q_dst[0], q_org[1], q_dst[1], hit_idx, hit_I, sq_org,
  * sq_dst, shadow, chain_local, chain_coef, depth, counters[0], counters[1], wq, cost[0], order[0],
  * cost[1], order[1], order_scratch. For tests of the sizing. */
-#define RT_WS_ARRAYS 20
+#define RT_WS_ARRAYS 22
 int rt_workspace_layout(int64_t cap, int32_t steps, int32_t lights, uint64_t *total_bytes,
                         uint64_t extents[2 * RT_WS_ARRAYS]);
 

@@ -29,7 +29,7 @@ RT_MAX_LIGHTS = 16        # lights held inline in rt_params; more through rt_par
 RT_LIGHTS_LIMIT = 65536
 RT_TRIAL_INFO_FIELDS, RT_MAX_TRIALS = 7, 10
 SAMPLES_RGB, SAMPLES_RAY_RGB = 3, 9   # rt_trace_frame_samples record layouts
-RT_WS_ARRAYS = 20   # rt_workspace_layout arrays
+RT_WS_ARRAYS = 22   # rt_workspace_layout arrays
 
 AMBIENT, DIFFUSE, SPECULAR, REFLECTION, SHADOWS, REFRACTION = (1 << i for i in range(6))
 ALL_FEATURES = 0x3F
@@ -52,6 +52,7 @@ TUNE_ADOPT_ORDER = 32
 TUNE_INFLIGHT_DYNAMIC = 33
 TUNE_INFLIGHT_STREAMS = 34
 TUNE_QUAD_WALK = 35
+TUNE_MOTION_ORDER = 36
 MAX_FRAMES_PER_CALL = 4   # RT_MAX_FRAMES_PER_CALL
 BVH_INFO_FIELDS = 7
 STOCHASTIC = 1 << 8

@@ -336,7 +336,8 @@ class Scene:
              "pixel_order": _capi.TUNE_PIXEL_ORDER, "dyn_group": _capi.TUNE_DYN_GROUP,
              "shadow_helpers": _capi.TUNE_SHADOW_HELPERS, "frames_in_flight": _capi.TUNE_FRAMES_IN_FLIGHT,
              "adopt_order": _capi.TUNE_ADOPT_ORDER, "inflight_dynamic": _capi.TUNE_INFLIGHT_DYNAMIC,
-             "inflight_streams": _capi.TUNE_INFLIGHT_STREAMS, "quad_walk": _capi.TUNE_QUAD_WALK}[knob]
+             "inflight_streams": _capi.TUNE_INFLIGHT_STREAMS, "quad_walk": _capi.TUNE_QUAD_WALK,
+             "motion_order": _capi.TUNE_MOTION_ORDER}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
 
     def trials(self) -> dict:

@@ -107,7 +107,7 @@ def test_tune_knobs_validate_ranges(tmp_path):
                             ("cold_estimate", (0, 1, 2), (3, -1)),
                             ("steal_half", (0, 512, 65535), (-1, 65536)), ("steal_quarter", (-1, 0, 8, 4096), (-2, 4097)),
                             ("split_eighth", (0, 64, 4096), (-1, 4097)), ("prio_batches", (0, 64, 1 << 30), (-1,)),
-                            ("shadow_helpers", (0, 1, 2), (3, -1)), ("frames_in_flight", (1, 2, 4), (0, 5)), ("pipes", (1, 4), (0, 5))]:
+                            ("shadow_helpers", (0, 1, 2), (3, -1)), ("quad_walk", (0, 1), (2, -1)), ("motion_order", (0, 1), (2, -1)), ("frames_in_flight", (1, 2, 4), (0, 5)), ("pipes", (1, 4), (0, 5))]:
         for v in good:
             s.tune(knob, v)
         for v in bad:
@@ -138,7 +138,7 @@ def test_workspace_layout_covers_every_array(cap, steps, lights):
     need = [cap * 16] * 4 + [cap * 4, cap * 16, cap * L * 16, cap * L * 16, cap * L, cap * steps * 16,
                              cap * steps * 16, cap, 4 * 2 * 4096, 4 * 2 * 4096, 4 * 2 * steps * 128]
     nbatch = max((cap + spb - 1) // spb for spb in [(64 // s) * s for s in range(1, 65)])
-    need += [4 * nbatch] * 4 + [4 * 128]
+    need += [4 * nbatch] * 4 + [4 * 128] + [4 * nbatch] * 2   # (+ a moving view's dilated costs and cells)
     assert len(need) == _capi.RT_WS_ARRAYS
     end = 0
     for (off, size), n in zip(ext, need):
