@@ -120,6 +120,8 @@ def parse():
                     help="N=1: also time a moving view, each frame the view turned by this many degrees more "
                          "(scenes.orbit_corners; 0 = skip): config.orbit")
     ap.add_argument("--no-multi-frame", action="store_true", help="skip the rt_render_frames_device leg")
+    ap.add_argument("--frames-per-call", type=int, default=4,
+                    help="N=1 frame path: frames of the view per rt_render_frames_device call (one chain launch), 1-4")
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
                     help="extra launch-shape knob (Scene.tune), e.g. shadow_virtual=-1; repeatable")
     return ap.parse_args()
@@ -212,7 +214,7 @@ def main():
             self.index = torch.as_tensor(self.plan.gather_index(), device=dev)
             if frame_path:
                 self.fbufs = [torch.zeros(HEIGHT * WIDTH * 3, dtype=torch.uint8, device=dev)
-                              for _ in range(max(2, args.inflight))]
+                              for _ in range(max(2, args.inflight, 2 * args.frames_per_call))]
                 # frames in flight: frame i on stream i % F (the first is the bench's stream). (Streams on
                 # hardware queues of their own, CU-masked, made the frames overlap worse: 0.43-0.52 vs
                 # 0.35 ms per C4 frame, profiles/r05e_ab_rtstreams.txt)
@@ -229,6 +231,8 @@ def main():
             else:
                 self.frames_out = [torch.zeros(1, dtype=torch.uint8, device=dev)] * 2
             self.fif = 1   # frames in flight of the current run (the timed run sets args.inflight)
+            self.fpc = 1   # frames per call (rt_render_frames_device; the timed run sets --frames-per-call)
+            self.total = 0   # frames of the current run's timed steps (frame path: steps are calls of fpc frames)
             self.nfin = 0
             self.pending = []
             # rank 0 un-permutes on a side stream, so the next step's render is not queued behind it
@@ -270,10 +274,22 @@ def main():
                                     gathered.numel(), out.data_ptr(), out.numel(), self.side.cuda_stream)
             return out.view(self.plan.frames, HEIGHT, WIDTH, 3)
 
-        def step(self, i):
+        def render_call(self, i, k):
+            """Call i of a multi-frame run: k frames of the view in one rt_render_frames_device call
+            (one chain launch) into buffers (i % 2) * fpc ..., on stream i % F."""
+            base = (i % 2) * self.fpc
+            st = self.fstreams[i % self.fif]
+            bufs = self.fbufs[base:base + k]
+            scene.render_frames_device([cparams] * k, TILE, TILE, [b.data_ptr() for b in bufs], bufs[0].numel(), st.cuda_stream)
+            return bufs[-1]
+
+        def step(self, i, k=1):
             """Render step i, start its gather (async, on the collective's stream) and finish step
-            i-1's: the gather of one step overlaps the next step's render."""
+            i-1's: the gather of one step overlaps the next step's render. Frame path with fpc > 1:
+            step i is a call of k frames."""
             if self.single:
+                if self.fpc > 1:
+                    return self.render_call(i, k).view(1, HEIGHT, WIDTH, 3)
                 return self.render_once(i).view(1, HEIGHT, WIDTH, 3)
             if rtcomm is not None:   # render + RCCL gather + un-permute, all inside the library
                 out = self.frames_out[i % 2]
@@ -296,9 +312,13 @@ def main():
 
         def run(self, steps, warmup):
             """warmup untimed steps, then `steps` timed ones between barriers + device syncs;
-            returns (max-over-ranks seconds, last frames)."""
+            returns (max-over-ranks seconds, last frames). Frame path with fpc > 1: `steps` frames
+            as calls of fpc frames (the last call the remainder); self.total = frames timed."""
+            calls = [self.fpc] * (steps // self.fpc) + ([steps % self.fpc] if steps % self.fpc else []) \
+                if (self.single and self.fpc > 1) else [1] * steps
+            self.total = sum(calls)
             for i in range(warmup):
-                self.step(i)
+                self.step(i, self.fpc)
             self.drain()
             torch.cuda.synchronize(dev)
             if world > 1:
@@ -306,8 +326,8 @@ def main():
             torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
             frames = None
-            for i in range(steps):
-                f = self.step(i)
+            for i, k in enumerate(calls):
+                f = self.step(i, k)
                 frames = f if f is not None else frames
             f = self.drain()   # the last step's gather + un-permute stay inside the timed region
             frames = f if f is not None else frames
@@ -360,26 +380,38 @@ def main():
         scene.tune("frames_in_flight", inflight)
         main_run.fif = inflight
     calib = calibrate(inflight)
+    fpc = max(1, min(args.frames_per_call, 4)) if main_run.single else 1
+    main_run.fpc = fpc
     # ---- timed region (the metric) ----
     elapsed, frames = main_run.run(args.steps, args.warmup * inflight)
+    main_run.fpc = 1
     # the last timed frame, kept before any later leg reuses its buffer: the in-run parity check
     # (cpu_baseline) reads this copy
     timed_last = frames.clone() if frames is not None else None
     torch.cuda.synchronize(dev)
-    timed_last_what = (f"timed step {args.steps - 1} of {args.steps}: stream {(args.steps - 1) % inflight} and render "
-                       f"pipeline {(args.steps - 1) % inflight} of {inflight} in flight" if main_run.single else
-                       f"timed step {args.steps - 1} of {args.steps} (the assembled frame on rank 0)")
-    one_in_flight = None
-    value_mode = f"{inflight}_in_flight" if inflight > 1 else "one_in_flight"
-    if inflight > 1:   # the same frames one at a time (each frame's own latency, back to back)
+    timed_last_what = (f"the last frame of the last timed call ({fpc} frames per call, {inflight} call(s) in flight)"
+                       if main_run.single else f"timed step {args.steps - 1} of {args.steps} (the assembled frame on rank 0)")
+    one_in_flight = in_flight = None
+    value_mode = (f"{fpc}_frames_per_call" if fpc > 1 else "") + (f"{'_' if fpc > 1 else ''}{inflight}_in_flight" if inflight > 1 else "")
+    value_mode = value_mode or "one_in_flight"
+    if main_run.single and (inflight > 1 or fpc > 1):   # the same frames one at a time (each frame's own latency)
         scene.tune("frames_in_flight", 1)
         main_run.fif = 1
         el1, _ = main_run.run(args.steps, args.warmup)
         one_in_flight = {"ms_per_step": round(el1 / args.steps * 1e3, 3),
                          "value": round(rays_per_step * args.steps / el1 / 1e6, 4),
-                         "what": "the same timed loop with one frame in flight (each launch waits for the previous frame)"}
-        # the line's value is the configured mode's (--inflight, chosen before the run); the same K
-        # frames one at a time are reported beside it
+                         "what": "the same timed loop with one frame per call and one in flight (each launch waits for "
+                                 "the previous frame)"}
+        if fpc > 1:   # and one frame per call, two calls in flight on two streams (round 4's headline mode)
+            scene.tune("frames_in_flight", 2)
+            main_run.fif = 2
+            el2, _ = main_run.run(args.steps, args.warmup * 2)
+            in_flight = {"ms_per_step": round(el2 / args.steps * 1e3, 3), "value": round(rays_per_step * args.steps / el2 / 1e6, 4),
+                         "what": "one frame per call, two frames in flight on alternating streams (RT_TUNE_FRAMES_IN_FLIGHT 2)"}
+            scene.tune("frames_in_flight", 1)
+            main_run.fif = 1
+        # the line's value is the configured mode's (--frames-per-call, --inflight: chosen before the run);
+        # the other modes over the same frames are reported beside it
 
     # ---- several frames per call (rt_render_frames_device): one launch, one stream ----
     multi_frame = None
@@ -442,32 +474,40 @@ def main():
                            "value": round(rays_per_step / world * args.steps / el2 / 1e6, 4)}
 
     # ---- kernel timing for the roofline (HIP events on the scene's launch stream) ----
-    def profile(steps, runner):
+    def profile(steps, runner, k=1):
         # kernel durations in isolation: one pipeline, so no launch shares the GPU with another;
-        # the same entry point as the timed loop, after it (so every launch is batch-ordered)
+        # the same entry point as the timed loop (k frames per call), after it (so every launch is
+        # batch-ordered)
+        def one(i):
+            if k > 1 and runner.single:
+                runner.fpc = k
+                runner.render_call(i, k)
+                runner.fpc = 1
+            else:
+                runner.render_once(i)
         scene.tune("pipes", 1)
-        runner.render_once()
+        one(0)
         torch.cuda.synchronize(dev)
         scene.reset_stats()
         scene.set_profiling(True)
         for i in range(max(steps, 1)):
-            runner.render_once(i)
+            one(i)
         torch.cuda.synchronize(dev)
         scene.set_profiling(False)
-        st = {k: scene.kernel_stats(k) for k in (KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME, KERNEL_CHAIN)}
+        st = {k_: scene.kernel_stats(k_) for k_ in (KERNEL_CLOSEST_HIT, KERNEL_SHADOW, KERNEL_SHADE, KERNEL_FRAME, KERNEL_CHAIN)}
         work = (0.0, 0.0, 0.0, 0.0)
         if scene.accel() == "bvh":   # work counters slow the kernels: count in a separate, untimed pass
             scene.reset_stats()
             scene.set_profiling(True, count_work=True)
             for i in range(max(steps, 1)):
-                runner.render_once(i)
+                one(i)
             torch.cuda.synchronize(dev)
             scene.set_profiling(False)
             work = scene.work_stats(KERNEL_CLOSEST_HIT) + scene.work_stats(KERNEL_SHADOW)
         scene.tune("pipes", args.pipes)
         return st, work
 
-    stats, (bvh_tests, bvh_visits, sh_bvh_tests, sh_bvh_visits) = profile(args.profile_steps, main_run)
+    stats, (bvh_tests, bvh_visits, sh_bvh_tests, sh_bvh_visits) = profile(args.profile_steps, main_run, fpc)
     # the wave batches of the latest (ordered) launch: the longest is the frame's critical path, the
     # floor of any split of one frame over N GPUs (DESIGN.md §9's strong-scaling model)
     batches = None
@@ -518,7 +558,7 @@ def main():
         total_rays = rays_per_step * args.steps
         value = total_rays / elapsed / 1e6
         queries = ch_tests / max(nt, 1)
-        per_rank_steps = args.profile_steps
+        per_rank_steps = args.profile_steps * fpc   # frames in the profiled launches
         traffic = traffic_src = None
         if args.accel == "bvh" and chain_launches > 0:
             # The chain kernel (every step of every sample per lane, RT_TUNE_CHAIN_FROM 0). Roof:
@@ -548,8 +588,8 @@ def main():
         # profiles/*_pmc_<workload>.json another one (tools/gpu_pmc.sh with WORKLOAD set)
         issue = None
         if args.accel == "bvh":
-            traffic, traffic_src = pmc_traffic(kname, args.workload)
-            pc, pc_src = pmc_counters(kname, "SQ_THREAD_CYCLES_VALU_per_launch", args.workload)
+            traffic, traffic_src = pmc_traffic(kname, args.workload, multi=fpc > 1)
+            pc, pc_src = pmc_counters(kname, "SQ_THREAD_CYCLES_VALU_per_launch", args.workload, multi=fpc > 1)
             if pc and avg_s > 0 and pc.get("SQ_INSTS_VALU_per_launch") and pc.get("SQ_ACTIVE_INST_VALU_per_launch"):
                 simds = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
                 iv = pc["SQ_INSTS_VALU_per_launch"]
@@ -564,7 +604,7 @@ def main():
                                  "per issued VALU instruction"}
         rocprof = None
         if args.accel == "bvh":   # the same kernel's mean in the committed rocprof run (cross-check of avg_launch_ms)
-            rp, rp_src = rocprof_mean(kname, args.workload)
+            rp, rp_src = rocprof_mean(kname, args.workload, multi=fpc > 1)
             if rp and rp["mean_us"] > 0:
                 ach = flops / max(ch_launches, 1) / (rp["mean_us"] * 1e-6) / 1e12
                 rocprof = dict(rp, source=rp_src, achieved=round(ach, 3), frac=round(ach / FP32_PEAK_TFLOPS, 4),
@@ -606,8 +646,8 @@ def main():
                 "frame_ms_per_gpu": round(elapsed / args.steps * 1e3, 3),
                 "frames_in_flight": inflight,
                 "value_mode": value_mode,
-                "value_mode_what": "value/ms_per_step come from the configured mode (--inflight frames in flight); "
-                                   "one_in_flight times the same K frames one at a time in the same run",
+                "value_mode_what": "value/ms_per_step come from the configured mode (--frames-per-call, --inflight); "
+                                   "one_in_flight (and in_flight) time the same K frames in the other modes in the same run",
                 "calibration_frames": calib,
                 "calibration_what": "frames rendered one at a time before the warm-up, over the F pipelines of the "
                                     "timed mode in turn, until pipeline 0's launch trials were decided (rt_scene_trials; "
@@ -617,6 +657,11 @@ def main():
                                          "while the previous frame's longest batches still run; ms_per_step is then "
                                          "the per-frame throughput time, one_in_flight the frame-after-frame time",
                 "one_in_flight": one_in_flight,
+                "in_flight": in_flight,
+                "frames_per_call": fpc,
+                "frames_per_call_what": "frames of the view rendered by one rt_render_frames_device call: one chain launch "
+                                        "whose wave tasks cycle over the frames (the frames overlap on one stream and one "
+                                        "hardware queue); ms_per_step = wall clock / frames",
                 "orbit": orbit,
                 "multi_frame": multi_frame,
                 "first_frame_ms": round(cold_ms, 3) if cold_ms is not None else None,
@@ -629,6 +674,7 @@ def main():
             },
             "roofline": {
                 "kernel": f"{kname} ({'every chain step: closest-hit, shadow and shade' if kname == 'k_chain' else 'primary + secondary queries'}, accel={args.accel})",
+                "frames_per_launch": fpc,
                 "bound": "valu",
                 "achieved": round(achieved, 3),
                 "peak": FP32_PEAK_TFLOPS,
@@ -807,7 +853,24 @@ def strong_model(t1_ms, crit_ms, shard_ms, frame_bytes, link_gbs=(50.0, 150.0), 
     return out
 
 
-def rocprof_mean(kernel: str, workload: str = "c4"):
+def timed_instantiation(kernel: str, name: str, multi: bool) -> bool:
+    """Whether profiled kernel `name` is the timed loop's instantiation of `kernel`: for k_chain<W,
+    kAnyHit, kCount, kInLane, kSteal, kQuad, kMulti>, not the counting one (kCount false), and the
+    multi-frame one (kMulti) exactly when the timed loop renders several frames per call (older
+    profiles, before kQuad/kMulti: any non-counting one)."""
+    if name == kernel:
+        return True
+    if not name.startswith(kernel + "<"):
+        return False
+    targs = [a.strip() for a in name[name.index("<") + 1:name.rindex(">")].split(",")]
+    if kernel != "k_chain":
+        return targs[-1] == "false"
+    if len(targs) > 2 and targs[2] != "false":
+        return False
+    return len(targs) < 7 or targs[6] == ("true" if multi else "false")
+
+
+def rocprof_mean(kernel: str, workload: str = "c4", multi: bool = False):
     """The committed rocprofv3 kernel-trace summary of `kernel` (tools/kernel_trace_summary.py over
     tools/gpu_final.sh's rocprof run of this bench, one frame in flight): the instantiation with the
     most launches, its mean duration after the first three launches. (dict, file) or (None, None)."""
@@ -819,7 +882,7 @@ def rocprof_mean(kernel: str, workload: str = "c4"):
             ks = json.load(open(f)).get("kernels", {})
         except (OSError, ValueError):
             continue
-        names = [n for n in ks if n == kernel or n.startswith(kernel + "<")]
+        names = [n for n in ks if timed_instantiation(kernel, n, multi)]
         if names:
             n = max(names, key=lambda k: ks[k].get("launches", 0))
             return {"instantiation": n, "launches": ks[n]["launches"], "mean_us": ks[n].get("mean_after_first_3_us", ks[n]["mean_us"])}, \
@@ -827,15 +890,15 @@ def rocprof_mean(kernel: str, workload: str = "c4"):
     return None, None
 
 
-def pmc_traffic(kernel: str, workload: str = "c4"):
+def pmc_traffic(kernel: str, workload: str = "c4", multi: bool = False):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary of `workload`
     (profiles/*_pmc.json for C4, profiles/*_pmc_<workload>.json otherwise; written by
     tools/pmc_summary.py from separate rocprofv3 --pmc passes of this bench command)."""
-    c, src = pmc_counters(kernel, "traffic_bytes_per_launch", workload)
+    c, src = pmc_counters(kernel, "traffic_bytes_per_launch", workload, multi)
     return (c["traffic_bytes_per_launch"], src) if c else (None, None)
 
 
-def pmc_counters(kernel: str, need: str, workload: str = "c4"):
+def pmc_counters(kernel: str, need: str, workload: str = "c4", multi: bool = False):
     """The per-launch counters of `kernel` (its timed instantiation) from the newest committed PMC
     summary of `workload` that has counter `need`: (dict, file) or (None, None)."""
     import glob
@@ -847,12 +910,8 @@ def pmc_counters(kernel: str, need: str, workload: str = "c4"):
         except (OSError, ValueError):
             continue
         ks = d.get("kernels", {})
-        # the timed (non-counting) instantiation of the kernel: kCount is the third template argument
-        # of k_chain<W, kAnyHit, kCount, kInLane>, the last one of k_bvh_closest_hit<W, kCount>
-        def counting(n):
-            args = [a.strip() for a in n[n.index("<") + 1:n.rindex(">")].split(",")]
-            return args[2] if kernel == "k_chain" and len(args) > 2 else args[-1]
-        names = [n for n in ks if n == kernel or (n.startswith(kernel + "<") and counting(n) == "false")]
+        # the timed loop's instantiation of the kernel (timed_instantiation)
+        names = [n for n in ks if timed_instantiation(kernel, n, multi)]
         names.sort(key=lambda n: -ks[n].get("launches_in_pass", 0))
         for n in names:
             if need in ks[n]:

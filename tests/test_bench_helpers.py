@@ -1,0 +1,31 @@
+"""bench.py's bookkeeping helpers (CPU): which profiled kernel name is the timed loop's instantiation
+(the roofline's traffic, issue counters and rocprof mean must come from the kernel the headline runs),
+and the strong-scaling model's arithmetic."""
+import bench
+
+
+def test_timed_instantiation_picks_the_headline_kernel():
+    single = "k_chain<4, true, false, true, false, false, false>"
+    multi = "k_chain<4, true, false, true, false, false, true>"
+    counting = "k_chain<4, true, true, true, false, false, true>"
+    quad = "k_chain<4, true, false, true, false, true, false>"
+    assert bench.timed_instantiation("k_chain", single, multi=False)
+    assert not bench.timed_instantiation("k_chain", multi, multi=False)
+    assert bench.timed_instantiation("k_chain", multi, multi=True)
+    assert not bench.timed_instantiation("k_chain", single, multi=True)
+    assert not bench.timed_instantiation("k_chain", counting, multi=True)
+    assert not bench.timed_instantiation("k_chain", quad, multi=True)
+    # profiles from before the kQuad/kMulti parameters: any non-counting instantiation
+    assert bench.timed_instantiation("k_chain", "k_chain<4, true, false, true, false>", multi=True)
+    assert not bench.timed_instantiation("k_chain", "k_chain<4, true, true, true, false>", multi=False)
+    assert bench.timed_instantiation("k_bvh_closest_hit", "k_bvh_closest_hit<4, false>", multi=False)
+    assert not bench.timed_instantiation("k_chain", "k_chain_kernarg_probe", multi=False)
+
+
+def test_strong_model_bounds():
+    m = bench.strong_model(0.39, 0.38, 0.40, 1920 * 1080 * 3)
+    for n in (2, 4, 8):
+        r = m[f"n{n}"]
+        assert r["render_ms"] >= 0.38 and r["render_ms"] >= 0.39 / n
+        for bw in ("50GBs", "150GBs"):
+            assert r[bw]["pipelined_ms_per_frame"] <= r[bw]["latency_ms_per_frame"]
