@@ -118,13 +118,14 @@ extern "C" {
                                     path) finish sooner; a part then holds at most 16 samples of whole pixels
                                     (pf 1, 2, 4; otherwise the plain quarter tier). 0 (default): off.
                                     Placement only */
-#define RT_TUNE_MOTION_ORDER 36   /* 1 (default): a fused frame whose corner rays differ from the previous launch of its
-                                    pipeline over the same batches (a moving view: the trackball turned between
-                                    'r' presses) re-sorts the batch order after every launch, from the durations
-                                    dilated over the screen (each batch takes the longest duration within the
-                                    3 x 3 cells of 8 x 8 pixels around it), so a long batch that moved by a few
-                                    pixels is still near the head; 0: the static schedule (every
-                                    RT_TUNE_ORDER_EVERY launches, undilated). Placement only */
+#define RT_TUNE_MOTION_ORDER 36   /* r >= 1 (default 2): a fused frame whose corner rays differ from the previous
+                                    launch of its pipeline over the same batches (a moving view: the trackball
+                                    turned between 'r' presses) re-sorts the batch order after every launch,
+                                    from the durations dilated over the screen (each batch takes the longest
+                                    duration within the (2r + 1) x (2r + 1) cells of 8 x 8 pixels around it), so
+                                    a long batch that moved by a few pixels is still near the head; 0: the
+                                    static schedule (every RT_TUNE_ORDER_EVERY launches, undilated), 0-8.
+                                    Placement only */
 #define RT_TUNE_TOP_NODES 13     /* retired in r03 (0-85 accepted, no effect): an LDS copy of the four-wide
                                     tree's top levels; with float node rows loaded from global memory it
                                     measured slower (flat loads, 64-bit addresses) */

@@ -186,10 +186,10 @@ constexpr int kWaveBatch = 64;   // lanes per wave batch of the chain launch (on
 constexpr int kChainMaxLights = RT_MAX_LIGHTS;   // the chain launch reads its lights from its arguments; more: per-step kernels
 hipError_t launch_order_batches(const DevWork &w, int64_t nbatches, hipStream_t stream);
 // The same for a moving view (a fused frame launch g of fuse_spp samples per pixel): the durations
-// dilated over 3 x 3 cells of 8 x 8 pixels first (dil_cost: nbatches entries, cells: cells_cap entries
-// >= ceil(width / 8) x ceil(height / 8), else the plain sort).
-hipError_t launch_order_batches_moving(const DevWork &w, int64_t nbatches, const FrameGeom &g, int fuse_spp, uint32_t *dil_cost,
-                                       uint32_t *cells, int64_t cells_cap, hipStream_t stream);
+// dilated over (2 radius + 1)^2 cells of 8 x 8 pixels first (dil_cost: nbatches entries, cells: cells_cap
+// entries >= ceil(width / 8) x ceil(height / 8), else the plain sort).
+hipError_t launch_order_batches_moving(const DevWork &w, int64_t nbatches, const FrameGeom &g, int fuse_spp, int radius,
+                                       uint32_t *dil_cost, uint32_t *cells, int64_t cells_cap, hipStream_t stream);
 // A cold launch's batch scores (no measured order yet): one primary walk per wave batch of a fused
 // launch (g, fuse_spp, capacity as launch_chain's), scored into score[batch] for launch_order_batches.
 void launch_estimate(const DevScene &s, const ShadeParams &p, const FrameGeom &g, int fuse_spp, int64_t capacity,

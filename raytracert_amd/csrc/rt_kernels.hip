@@ -2878,7 +2878,7 @@ void launch_frame(const FrameGeom &g, const DevWork &w, uint8_t *out_u8, float *
 // A moving view's batch order (RT_TUNE_MOTION_ORDER): the durations of the previous view, dilated over
 // the screen, so a long batch that moved by a few pixels since is still near the head. Per batch its
 // duration (a split one's doubled, as order_bucket counts it) goes into the 8 x 8-pixel cell of its
-// middle sample (atomicMax), then each batch takes the maximum over the 3 x 3 cells around its own.
+// middle sample (atomicMax), then each batch takes the maximum over the (2r + 1)^2 cells around its own.
 __device__ __forceinline__ uint32_t order_cost(uint32_t c) { return (c & kCostSplit) ? min((c & ~kCostSplit) * 2u, ~kCostSplit) : c; }
 __device__ __forceinline__ int order_cell(const FrameGeom &g, int spb, int nq, int b, int cells_x) {
     const int first = b * spb, n = min(spb, nq - first);
@@ -2895,21 +2895,21 @@ __global__ __launch_bounds__(kBlock) void k_order_cells(const uint32_t *__restri
     atomicMax(&cells[order_cell(g, spb, nq, b, cells_x)], order_cost(cost[b]));
 }
 __global__ __launch_bounds__(kBlock) void k_order_dilate(int n, const FrameGeom g, int spb, int nq, int cells_x, int cells_y,
-                                                         const uint32_t *__restrict__ cells, uint32_t *__restrict__ out) {
+                                                         int radius, const uint32_t *__restrict__ cells, uint32_t *__restrict__ out) {
     const int b = static_cast<int>(blockIdx.x) * kBlock + static_cast<int>(threadIdx.x);
     if (b >= n) return;
     const int c = order_cell(g, spb, nq, b, cells_x), cx = c % cells_x, cy = c / cells_x;
     uint32_t m = 0;
-    for (int dy = -1; dy <= 1; ++dy)
-        for (int dx = -1; dx <= 1; ++dx) {
+    for (int dy = -radius; dy <= radius; ++dy)
+        for (int dx = -radius; dx <= radius; ++dx) {
             const int x = cx + dx, y = cy + dy;
             if (x >= 0 && x < cells_x && y >= 0 && y < cells_y) m = max(m, cells[y * cells_x + x]);
         }
     out[b] = m;
 }
 
-hipError_t launch_order_batches_moving(const DevWork &w, int64_t nbatches, const FrameGeom &g, int fuse_spp, uint32_t *dil_cost,
-                                       uint32_t *cells, int64_t cells_cap, hipStream_t stream) {
+hipError_t launch_order_batches_moving(const DevWork &w, int64_t nbatches, const FrameGeom &g, int fuse_spp, int radius,
+                                       uint32_t *dil_cost, uint32_t *cells, int64_t cells_cap, hipStream_t stream) {
     if (nbatches <= 0) return hipSuccess;
     const FrameGeom gd = with_divisors(g);
     const int cells_x = (g.width + 7) / 8, cells_y = (g.height + 7) / 8;
@@ -2919,7 +2919,8 @@ hipError_t launch_order_batches_moving(const DevWork &w, int64_t nbatches, const
     hipError_t e = hipMemsetAsync(cells, 0, sizeof(uint32_t) * static_cast<size_t>(cells_x) * cells_y, stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_order_cells, dim3(grid_for(n)), dim3(kBlock), 0, stream, w.batch_cost, n, gd, spb, nq, cells_x, cells);
-    hipLaunchKernelGGL(k_order_dilate, dim3(grid_for(n)), dim3(kBlock), 0, stream, n, gd, spb, nq, cells_x, cells_y, cells, dil_cost);
+    hipLaunchKernelGGL(k_order_dilate, dim3(grid_for(n)), dim3(kBlock), 0, stream, n, gd, spb, nq, cells_x, cells_y, radius, cells,
+                       dil_cost);
     DevWork wd = w;
     wd.batch_cost = dil_cost;
     return launch_order_batches(wd, nbatches, stream);
