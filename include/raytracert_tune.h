@@ -106,7 +106,8 @@ extern "C" {
                                     trials timed the chosen shape with them within 3% of the choice (the next
                                     frame's blocks then fill the slots the previous frame's tail frees; block
                                     dispatch runs two frames side by side from their first blocks: C4 0.387
-                                    -> 0.377 ms per frame); 0: always the trials' distribution. Placement only */
+                                    -> 0.377 ms per frame); 2: also multi-frame launches (rt_render_frames_device)
+                                    one in flight; 0: always the trials' distribution. Placement only */
 #define RT_TUNE_INFLIGHT_STREAMS 34 /* 1: with RT_TUNE_FRAMES_IN_FLIGHT > 1, a single-pipeline call runs on its
                                     pipeline's own stream (forked from the caller's stream and joined back),
                                     so two frames in flight overlap whichever hardware queues the caller's
