@@ -194,3 +194,20 @@ def test_oversized_sample_counts_are_rejected(workdir, gpu_available):
         assert ei.value.code == _capi.RT_E_ARG
         u8, _, _ = sc.render(R.RenderParams(width=64, height=36, pf=2, max_lvl=1, lights=lights), 0, 0, 8, 8)
         assert u8.shape == (8, 8, 3)   # the scene still renders afterwards
+
+
+def test_tile_workspace_over_budget_is_nomem(workdir, gpu_available):
+    """Near the light limit: 65,536 lights x one 16x16 tile at pf 7 (12,544 samples,
+    inside the int32 queue range) needs ~27 GB of render workspace for that one tile, over the 24 GB
+    budget: a clean RT_E_NOMEM before anything is allocated or launched, and the scene renders after."""
+    import torch
+    from raytracert_amd import _capi
+    lights = [(0.001 * (i % 256), 0.001 * (i // 256), 4.0) for i in range(65536)]
+    with R.Scene.load(scene_path("syn:F3", workdir), device=0) as sc:
+        buf = torch.zeros(16 * 16 * 3, dtype=torch.uint8, device="cuda:0")
+        p = R.RenderParams(width=16, height=16, pf=7, max_lvl=1, lights=lights)
+        with pytest.raises(R.RtError) as ei:
+            sc.render_tiles_device(p, 16, 16, 0, 1, buf.data_ptr(), buf.numel())
+        assert ei.value.code == _capi.RT_E_NOMEM
+        u8, _, _ = sc.render(R.RenderParams(width=64, height=36, pf=2, max_lvl=1, lights=LIGHT_SETS[16]), 0, 0, 8, 8)
+        assert u8.shape == (8, 8, 3)
