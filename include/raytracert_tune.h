@@ -106,8 +106,10 @@ extern "C" {
                                     trials timed the chosen shape with them within 3% of the choice (the next
                                     frame's blocks then fill the slots the previous frame's tail frees; block
                                     dispatch runs two frames side by side from their first blocks: C4 0.387
-                                    -> 0.377 ms per frame); 2: also multi-frame launches (rt_render_frames_device)
-                                    one in flight; 0: always the trials' distribution. Placement only */
+                                    -> 0.377 ms per frame). The same for multi-frame launches (rt_render_frames_device),
+                                    whose tasks of K frames fill the slots a frame's tail frees (C4, 4 frames per
+                                    call: 0.3445 -> 0.3412 ms per frame, profiles/r05i_ab_multi_c4.txt);
+                                    0: always the trials' distribution. Placement only */
 #define RT_TUNE_INFLIGHT_STREAMS 34 /* 1: with RT_TUNE_FRAMES_IN_FLIGHT > 1, a single-pipeline call runs on its
                                     pipeline's own stream (forked from the caller's stream and joined back),
                                     so two frames in flight overlap whichever hardware queues the caller's
@@ -119,14 +121,15 @@ extern "C" {
                                     path) finish sooner; a part then holds at most 16 samples of whole pixels
                                     (pf 1, 2, 4; otherwise the plain quarter tier). 0 (default): off.
                                     Placement only */
-#define RT_TUNE_MOTION_ORDER 36   /* r >= 1 (default 2): a fused frame whose corner rays differ from the previous
+#define RT_TUNE_MOTION_ORDER 36   /* r >= 1 (default 1): a fused frame whose corner rays differ from the previous
                                     launch of its pipeline over the same batches (a moving view: the trackball
                                     turned between 'r' presses) re-sorts the batch order after every launch,
                                     from the durations dilated over the screen (each batch takes the longest
                                     duration within the (2r + 1) x (2r + 1) cells of 8 x 8 pixels around it), so
                                     a long batch that moved by a few pixels is still near the head; 0: the
                                     static schedule (every RT_TUNE_ORDER_EVERY launches, undilated), 0-8.
-                                    Placement only */
+                                    C4 orbit at 0.25 deg per frame, one in flight: r 1 0.456-0.461 ms, 2 0.50-0.52,
+                                    3 0.54, 0 0.486 (profiles/r05h_orbit_ab.txt). Placement only */
 #define RT_TUNE_TOP_NODES 13     /* retired in r03 (0-85 accepted, no effect): an LDS copy of the four-wide
                                     tree's top levels; with float node rows loaded from global memory it
                                     measured slower (flat loads, 64-bit addresses) */
