@@ -806,6 +806,33 @@ def orbit_leg(scene, run, W, H, PF, MAX_LVL, LIGHTS, flags, args, inflight, obj,
     last = run.fbufs[(K - 1) % max(2, inflight)].clone().view(H, W, 3)
     torch.cuda.synchronize(dev)
     el1 = loop(1, warm, K) if inflight > 1 else el
+    # a camera path rendered --frames-per-call consecutive views per rt_render_frames_device call (one
+    # chain launch over the views, one call at a time); the call's last view re-rendered alone must match
+    fpc = args.frames_per_call if not args.no_multi_frame else 1
+    multi = None
+    if fpc > 1:
+        calls = max(K // fpc, 1)
+        scene.tune("frames_in_flight", 1)
+        st = run.fstreams[0]
+
+        def mcall(first, i):
+            bufs = run.fbufs[(i % 2) * fpc:(i % 2) * fpc + fpc]
+            scene.render_frames_device(views[first + i * fpc:first + i * fpc + fpc], TILE, TILE,
+                                       [b.data_ptr() for b in bufs], bufs[0].numel(), st.cuda_stream)
+            return bufs[-1]
+        for i in range(max(warm // fpc, 2)):
+            mcall(0, i)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(calls):
+            lastb = mcall(warm, i)
+        torch.cuda.synchronize(dev)
+        elm = time.perf_counter() - t0
+        alone = torch.zeros_like(lastb)
+        scene.render_frame_device(views[warm + calls * fpc - 1], TILE, TILE, alone.data_ptr(), alone.numel(), st.cuda_stream)
+        torch.cuda.synchronize(dev)
+        multi = {"frames_per_call": fpc, "views_timed": calls * fpc, "ms_per_step": round(elm / (calls * fpc) * 1e3, 3),
+                 "last_view_equals_alone": bool(torch.equal(lastb, alone))}
     rays = 0
     for k in range(warm, warm + K):
         fb = run.fbufs[0]
@@ -820,6 +847,7 @@ def orbit_leg(scene, run, W, H, PF, MAX_LVL, LIGHTS, flags, args, inflight, obj,
             "frames_in_flight": inflight,
             "ms_per_step": round(el / K * 1e3, 3), "value": round(rays / el / 1e6, 4),
             "one_in_flight": {"ms_per_step": round(el1 / K * 1e3, 3), "value": round(rays / el1 / 1e6, 4)},
+            "views_per_call": (dict(multi, value=round(rays / K / (elm / multi["views_timed"]) / 1e6, 4)) if multi else None),
             "rays_per_frame_mean": round(rays / K), "unit": "Mrays/s",
             "_last": (last, corners[warm + K - 1])}
 
