@@ -218,7 +218,7 @@ def main():
                 # frames in flight: frame i on stream i % F (the first is the bench's stream). (Streams on
                 # hardware queues of their own, CU-masked, made the frames overlap worse: 0.43-0.52 vs
                 # 0.35 ms per C4 frame, profiles/r05e_ab_rtstreams.txt)
-                self.fstreams = [stream] + [torch.cuda.Stream(dev) for _ in range(max(args.inflight, 1) - 1)]
+                self.fstreams = [stream] + [torch.cuda.Stream(dev) for _ in range(max(args.inflight, 2) - 1)]   # (>= 2: the in-flight leg)
                 # a new stream's first command initialises it (~6 ms of host time on this image): done
                 # here, at setup, not at the warm-up's second frame, where it left the GPU idle just
                 # before the timed frames (they then ran ~5% slow for ~25 frames)
