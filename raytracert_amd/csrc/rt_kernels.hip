@@ -2303,7 +2303,9 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
                 r[0] = org.x; r[1] = org.y; r[2] = org.z; r[3] = dst.x; r[4] = dst.y; r[5] = dst.z;
             }
             lvl = 0;
-            sample = j;
+            // (a multi-frame launch: frame fr's chain records past the LDS ones at j + fr x nq; the host sized
+            // the workspace for nfr x nq samples, rt_capi.cpp frames_workspace_cap)
+            sample = nfr > 1 ? j + fr * nq : j;
         } else {
             if (!own) return;
             const float4 qo = wb.q_org[first & 1][j], qd = wb.q_dst[first & 1][j];
