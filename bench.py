@@ -121,7 +121,7 @@ def parse():
                          "(scenes.orbit_corners; 0 = skip): config.orbit")
     ap.add_argument("--no-multi-frame", action="store_true", help="skip the rt_render_frames_device leg")
     ap.add_argument("--frames-per-call", type=int, default=4,
-                    help="N=1 frame path: frames of the view per rt_render_frames_device call (one chain launch), 1-4")
+                    help="N=1 frame path: frames of the view per rt_render_frames_device call (one chain launch), 1-8")
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
                     help="extra launch-shape knob (Scene.tune), e.g. shadow_virtual=-1; repeatable")
     return ap.parse_args()
@@ -380,7 +380,7 @@ def main():
         scene.tune("frames_in_flight", inflight)
         main_run.fif = inflight
     calib = calibrate(inflight)
-    fpc = max(1, min(args.frames_per_call, 4)) if main_run.single else 1
+    fpc = max(1, min(args.frames_per_call, 8)) if main_run.single else 1
     main_run.fpc = fpc
     # ---- timed region (the metric) ----
     elapsed, frames = main_run.run(args.steps, args.warmup * inflight)
@@ -746,11 +746,11 @@ def multiframe_leg(scene, run, cparams, W, H, args, rays_per_frame, dev):
     on one stream, and K = 2 with two calls in flight (RT_TUNE_FRAMES_IN_FLIGHT 2, two streams). Every
     frame is fully rendered; ms_per_frame = wall clock / frames."""
     import torch
-    K_MAX = 4
+    K_MAX = 8
     bufs = [torch.zeros(H * W * 3, dtype=torch.uint8, device=dev) for _ in range(2 * K_MAX)]
     out = {"what": "K frames of the view per rt_render_frames_device call (one chain launch whose wave tasks cycle "
                    "over the frames), calls back to back; every frame fully rendered"}
-    for K, fif in ((2, 1), (4, 1), (2, 2)):
+    for K, fif in ((2, 1), (4, 1), (8, 1), (2, 2), (4, 2)):
         scene.tune("frames_in_flight", fif)
         calls = max(args.steps // K, 2)
 

@@ -234,13 +234,13 @@ int rt_render_frame_device(rt_scene *scene, const rt_params *params, int32_t til
 /* Several frames of one frame geometry, each its own view: params[f] (f < n_frames) may differ from
  * params[0] in their corner rays only (the trackball turned between 'r' presses, main.cpp:355-358), and
  * frame f goes row-major into the DEVICE buffer d_out_u8[f] (each out_capacity bytes). One chain launch
- * renders all of them when the frame is one batch of the four-wide tree and max_lvl <= 3 (C4, C5): its wave tasks cycle
+ * renders all of them when the frame is one batch of the four-wide tree (C4, C5, the reference's defaults): its wave tasks cycle
  * over the frames, so the frames' longest batches start side by side and the short ones of each fill
  * the slots the others' tails free, on one stream and one hardware queue (the overlap frames in flight
  * on two streams get, without depending on the runtime placing those streams on different hardware
  * queues). Otherwise the frames render one after another. Bytes equal the frames rendered one at a
  * time. counts: the sum over the frames. Stream semantics as rt_render_tiles_device. */
-#define RT_MAX_FRAMES_PER_CALL 4
+#define RT_MAX_FRAMES_PER_CALL 8
 int rt_render_frames_device(rt_scene *scene, const rt_params *params, int32_t n_frames, int32_t tile_w, int32_t tile_h,
                             void *const *d_out_u8, size_t out_capacity, void *stream, uint64_t counts[3]);
 int rt_render_tiles_device(rt_scene *scene, const rt_params *params, int32_t tile_w, int32_t tile_h,

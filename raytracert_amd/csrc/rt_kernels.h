@@ -39,7 +39,7 @@ struct FrameGeom {
 // differ only in their corner rays (views) and outputs. The launch's wave tasks cycle over the frames
 // (task t: frame t % count, the frame's own task t / count), so the frames' longest batches start side
 // by side and their short ones fill the slots the others' tails free, in one launch on one queue.
-constexpr int kMaxFramesPerLaunch = 4;
+constexpr int kMaxFramesPerLaunch = 8;
 struct FrameSet {
     int32_t count;                                  // 1: a single frame (the FrameGeom's corners and outputs)
     float corners[kMaxFramesPerLaunch][8][3];

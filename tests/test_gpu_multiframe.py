@@ -41,14 +41,14 @@ def test_frames_in_one_launch_equal_single_frames(name, knobs, workdir, gpu_avai
     wl = C4 if name == "c4" else REF
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev)
-    views = _views(wl, 4)
+    views = _views(wl, 8)
     with R.Scene.load(scene_path(wl["spec"], workdir), device=0) as sc:
         for k, v in knobs.items():
             sc.tune(k, v)
         singles = [_single(sc, torch, dev, p) for p in views]
         torch.cuda.synchronize(dev)
-        for it in range(12):   # cold, re-sorted and (after the trials) ordered launches; K = 2, 3, 4
-            K = 2 + it % 3
+        for it in range(12):   # cold, re-sorted and (after the trials) ordered launches; K = 2, 3, 4, 8
+            K = (2, 3, 4, 8)[it % 4]
             bufs = [torch.full((wl["h"] * wl["w"] * 3,), 7, dtype=torch.uint8, device=dev) for _ in range(K)]
             counts = sc.render_frames_device(views[:K], 16, 16, [b.data_ptr() for b in bufs], bufs[0].numel(), st.cuda_stream,
                                              want_counts=(it % 3 == 0))
@@ -58,7 +58,7 @@ def test_frames_in_one_launch_equal_single_frames(name, knobs, workdir, gpu_avai
             if counts is not None:
                 assert [int(x) for x in counts] == [sum(int(singles[f][1][k]) for f in range(K)) for k in range(3)]
         # the views are distinct, and one of them matches the oracle on a tile of its sphere region
-        assert len({s[0].cpu().numpy().tobytes().__hash__() for s in singles}) == 4
+        assert len({s[0].cpu().numpy().tobytes().__hash__() for s in singles}) == 8
         x0, y0 = (wl["w"] // 2) & ~15, (wl["h"] // 2) & ~15
         img = singles[3][0].cpu().numpy().reshape(wl["h"], wl["w"], 3)
         op = O.make_params(wl["w"], wl["h"], wl["pf"], wl["max_lvl"], lights=wl["lights"], corners=views[3].corners)
