@@ -30,12 +30,15 @@ RT_HD inline double sconst(double c) {
 RT_HD inline float spec_pow(float xf, float yf) {
     if (yf == 0.0f || xf == 1.0f) return 1.0f;                       // pow(x, ±0) = pow(1, y) = 1
     if (xf != xf || yf != yf) return xf + yf;                         // NaN
-    // negative bases (SpecularTerm is std::max(.., 0), so only -0 reaches here): C99 pow's sign
-    const bool y_int = std::fabs(yf) >= 16777216.0f || yf == std::trunc(yf);
-    const bool y_odd = std::fabs(yf) < 16777216.0f && y_int && std::fmod(yf, 2.0f) != 0.0f;
-    const bool neg = std::signbit(xf);
-    if (neg && xf != 0.0f && !y_int) return NAN;
-    const float sgn = neg && y_odd ? -1.0f : 1.0f;
+    // negative bases (SpecularTerm is std::max(.., 0), so only -0 reaches here): C99 pow's sign. The
+    // exponent's integer/odd tests (an fmod loop) run only for a negative base.
+    float sgn = 1.0f;
+    if (std::signbit(xf)) {
+        const bool y_int = std::fabs(yf) >= 16777216.0f || yf == std::trunc(yf);
+        const bool y_odd = std::fabs(yf) < 16777216.0f && y_int && std::fmod(yf, 2.0f) != 0.0f;
+        if (xf != 0.0f && !y_int) return NAN;
+        if (y_odd) sgn = -1.0f;
+    }
     xf = std::fabs(xf);
     if (xf == 1.0f) return sgn;
     const double y = static_cast<double>(yf);
