@@ -55,6 +55,8 @@ struct ShadeParams {
     float lights[RT_MAX_LIGHTS][3];     // the first RT_MAX_LIGHTS lights
     float cam[3];
     float pad;
+    float lnorm[RT_MAX_LIGHTS][3];      // diffuseOnly's lightpos.normalize() of the first lights (Vec3D.h:142-151),
+                                        // made on the host with the same float operations (shade_params)
     const float *light_ext;             // n_lights > RT_MAX_LIGHTS: all n_lights x 3 (device), else null
 };
 

@@ -1669,6 +1669,9 @@ __device__ __forceinline__ void offset_point(V3 &point, V3 dest) {   // addOffse
 #ifndef RT_HOIST_VIEW
 #define RT_HOIST_VIEW 0   // measured: C4 equal, C5 6.85 -> 6.89 ms (profiles/r04_ab_hoist_view.txt)
 #endif
+#ifndef RT_HOIST_LNORM
+#define RT_HOIST_LNORM 1   // diffuse's normalize(light position) from ShadeParams::lnorm (made on the host)
+#endif
 template <bool kInLane = false, bool kExtLights = true, typename Shadowed>
 __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadeParams &p, const DevWork &w, int step,
                                                int sample, V3 ray, int lvl, int idx, V3 P,
@@ -1706,7 +1709,8 @@ __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadePa
             V3 diffuse = mk(0, 0, 0);
             normalize(normal);
             V3 lp = L;
-            normalize(lp);
+            if (RT_HOIST_LNORM && (!kExtLights || l < RT_MAX_LIGHTS)) lp = mk(p.lnorm[l][0], p.lnorm[l][1], p.lnorm[l][2]);
+            else normalize(lp);
             diffuse = add(diffuse, scale(Kd, max_std(dot(normal, lp), 0.0f)));
             color = add(color, scale(diffuse, m.Tr));                // :349
         }
