@@ -80,7 +80,9 @@ struct ShadowSource {
 struct DevScene {
     const TriRec *tris;
     const uint32_t *tri_mat;
-    const float4 *normals;          // xyz = face normal
+    const float4 *normals;          // xyz = face normal; w = 1: ntab holds its normalize() states
+    const float4 *ntab;             // per face [N(n), N(N(n))] where N(N(N(n))) == N(n) bitwise (shade's
+                                    // repeated normal.normalize(), Vec3D.h:142-151), k_normal_table
     const DevMaterial *mats;
     const uint32_t *ties;           // powf(x,2) tie table
     int32_t nt, nm, n_ties, any_transparent;
@@ -200,6 +202,7 @@ void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *d
                            int32_t *idx, float4 *I, hipStream_t stream);
 // calculateNormals on the device (face normal per triangle into normals[i].xyz)
 void launch_face_normals(const float *xyz, const uint32_t *tri_v, int32_t nt, float4 *normals, hipStream_t stream);
+void launch_normal_table(float4 *normals, float4 *ntab, int32_t nt, hipStream_t stream);
 // Un-permute gathered tile shards ([nranks][slots][th][tw][3], tile g of the frames x T tiles in
 // rank g % nranks, slot g / nranks) into frames x height x width x 3 bytes; with slot0 / nslots, a
 // gather chunk holding slots [slot0, slot0 + nslots) of every rank ([nranks][nslots][th][tw][3]).

@@ -1667,10 +1667,15 @@ __device__ __forceinline__ void offset_point(V3 &point, V3 dest) {   // addOffse
 // and returns the secondary ray, if any. ray = dest - origin of the traced ray (:393);
 // is_shadowed(l) is isShadow's verdict for light l.
 #ifndef RT_HOIST_VIEW
-#define RT_HOIST_VIEW 0   // measured: C4 equal, C5 6.85 -> 6.89 ms (profiles/r04_ab_hoist_view.txt)
+#define RT_HOIST_VIEW 1   // r04 one frame per launch: C4 equal, C5 6.85 -> 6.89 ms (profiles/r04_ab_hoist_view.txt);
+                          // r05 multi-frame launches (VALU-bound): C4 0.3398 -> 0.3395, C5 6.637 -> 6.589 ms
+                          // (profiles/r05o_ab_shade.txt)
 #endif
 #ifndef RT_HOIST_LNORM
 #define RT_HOIST_LNORM 1   // diffuse's normalize(light position) from ShadeParams::lnorm (made on the host)
+#endif
+#ifndef RT_NORMAL_TABLE
+#define RT_NORMAL_TABLE 1  // the hit normal's normalize() states from DevScene::ntab (k_normal_table)
 #endif
 template <bool kInLane = false, bool kExtLights = true, typename Shadowed>
 __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadeParams &p, const DevWork &w, int step,
@@ -1682,7 +1687,15 @@ __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadePa
     sec.dst = mk(0, 0, 0);
     sec.lvl = -1;
     const int64_t ci = static_cast<int64_t>(step) * w.cap + sample;
-    V3 normal = ld3(sc.normals[idx]);                                // :394 (copy, mutated below)
+    const float4 nw = sc.normals[idx];
+    V3 normal = ld3(nw);                                             // :394 (copy, mutated below)
+    // normal.normalize() (:199, :213): from the face's tabled states when it has them (k_normal_table)
+    const bool tabled = RT_NORMAL_TABLE && nw.w != 0.0f;
+    int nstate = 0;
+    auto renormalize = [&]() {
+        if (tabled) { nstate ^= 1; normal = ld3(sc.ntab[2 * static_cast<int64_t>(idx) + (nstate ? 0 : 1)]); }
+        else normalize(normal);
+    };
     const uint32_t mi = sc.tri_mat[idx];
     const DevMaterial m = sc.mats[mi];                               // :396
     uint32_t kind = 0;
@@ -1707,7 +1720,7 @@ __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadePa
         if (shadowed) continue;
         if ((f & RT_DIFFUSE) && (m.flags & RT_HAS_KD)) {             // diffuseOnly :197-205
             V3 diffuse = mk(0, 0, 0);
-            normalize(normal);
+            renormalize();
             V3 lp = L;
             if (RT_HOIST_LNORM && (!kExtLights || l < RT_MAX_LIGHTS)) lp = mk(p.lnorm[l][0], p.lnorm[l][1], p.lnorm[l][2]);
             else normalize(lp);
@@ -1718,7 +1731,7 @@ __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadePa
             V3 spec = mk(0, 0, 0);
             V3 Vv = Vh;
             if (!RT_HOIST_VIEW) Vv = sub(mk(p.cam[0], p.cam[1], p.cam[2]), P);
-            normalize(normal);
+            renormalize();
             if (!RT_HOIST_VIEW) normalize(Vv);
             V3 Lv = sub(L, P);
             normalize(Lv);
@@ -2544,6 +2557,27 @@ __global__ __launch_bounds__(kBlock) void k_face_normals(const float *__restrict
     normals[i] = make_float4(n.x, n.y, n.z, 0.0f);
 }
 
+// shade() normalises the hit's normal in place once per diffuse and once per specular term of every lit
+// light (diffuseOnly / blinnPhongSpecularOnly, raytracing.cpp:199,213): the k-th state of a face's normal
+// is N^k(n). Where N(N(N(n))) == N(n) bit for bit (the states alternate from the first on: nearly every
+// face), the two states are tabled once here with the kernels' own normalize, and shading picks state k
+// by its parity instead of normalising again (w = 1 marks the face; otherwise shading normalises).
+__global__ __launch_bounds__(kBlock) void k_normal_table(float4 *__restrict__ normals, float4 *__restrict__ ntab, int32_t nt) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= nt) return;
+    const float4 n0 = normals[i];
+    V3 n1 = mk(n0.x, n0.y, n0.z);
+    normalize(n1);
+    V3 n2 = n1;
+    normalize(n2);
+    V3 n3 = n2;
+    normalize(n3);
+    const bool ok = as_int(n3.x) == as_int(n1.x) && as_int(n3.y) == as_int(n1.y) && as_int(n3.z) == as_int(n1.z);
+    ntab[2 * i] = make_float4(n1.x, n1.y, n1.z, 0.0f);
+    ntab[2 * i + 1] = make_float4(n2.x, n2.y, n2.z, 0.0f);
+    normals[i] = make_float4(n0.x, n0.y, n0.z, ok ? 1.0f : 0.0f);
+}
+
 // rayIntersectTriangle (raytracing.cpp:99-154) for n independent (ray, triangle) pairs, every
 // step in the reference's order; unlike intersectMesh's use of it there is no distance compare, so
 // a hit whose point is NaN or infinite is still reported, as the reference returns true for it.
@@ -2962,6 +2996,11 @@ void launch_intersect_only(const DevScene &s0, const float4 *org, const float4 *
         return;
     }
     hipLaunchKernelGGL(k_intersect_only, dim3(grid_for(n)), dim3(kBlock), 0, stream, s0.tris, s0.nt, org, dst, n, idx, I);
+}
+
+void launch_normal_table(float4 *normals, float4 *ntab, int32_t nt, hipStream_t stream) {
+    if (nt <= 0) return;
+    hipLaunchKernelGGL(k_normal_table, dim3(grid_for(nt)), dim3(kBlock), 0, stream, normals, ntab, nt);
 }
 
 void launch_face_normals(const float *xyz, const uint32_t *tri_v, int32_t nt, float4 *normals, hipStream_t stream) {
