@@ -1675,7 +1675,10 @@ __device__ __forceinline__ void offset_point(V3 &point, V3 dest) {   // addOffse
 #define RT_HOIST_LNORM 1   // diffuse's normalize(light position) from ShadeParams::lnorm (made on the host)
 #endif
 #ifndef RT_NORMAL_TABLE
-#define RT_NORMAL_TABLE 1  // the hit normal's normalize() states from DevScene::ntab (k_normal_table)
+#define RT_NORMAL_TABLE 0  // the hit normal's normalize() states from DevScene::ntab (k_normal_table). Measured
+                           // (multi-frame launches): C5 (4 lights) 6.594 -> 6.566 ms, C4 (2 lights) 0.3400 ->
+                           // 0.3410 ms (profiles/r05p_ab_normal_table.txt): the table's loads cost about what the
+                           // normalisations did at 2 lights; off for the C4 headline
 #endif
 template <bool kInLane = false, bool kExtLights = true, typename Shadowed>
 __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadeParams &p, const DevWork &w, int step,
