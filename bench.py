@@ -972,6 +972,9 @@ def dropin_loop(obj, wl):
     return {"what": "main.cpp:355-395 unchanged (performRayTracing per sub-sample) over the drop-in header, "
                     f"{wl['width']}x{wl['height']} pf {wl['pf']} = {n} calls",
             "loop_ms": loop_ms, "first_loop_ms": float(fr[0][10]), "render_image_ms": float(fr[2][7]),
+            "frame_trace_ms": float(fr[1][12]), "first_frame_trace_ms": float(fr[0][12]),
+            "frame_trace_what": "the loop's first performRayTracing call, which traces the whole frame on the GPU "
+                                "(rt_trace_frame_samples) and copies every sub-sample's ray and colour to pinned host memory",
             "host_floor_ms": min(floor) if floor else None,
             "host_floor_what": "the same loop with performRayTracing replaced by a function that only reads its "
                                "arguments: the unchanged loop's own cost (two divisions and ~60 flops per call)",
