@@ -230,6 +230,7 @@ def main():
                 self.frames_out = [torch.zeros(frames * HEIGHT * WIDTH * 3, dtype=torch.uint8, device=dev) for _ in range(2)]
             else:
                 self.frames_out = [torch.zeros(1, dtype=torch.uint8, device=dev)] * 2
+            self.kstep = 1   # N > 1 weak: steps per render call (the plan holds kstep x N frames)
             self.fif = 1   # frames in flight of the current run (the timed run sets args.inflight)
             self.fpc = 1   # frames per call (rt_render_frames_device; the timed run sets --frames-per-call)
             self.total = 0   # frames of the current run's timed steps (frame path: steps are calls of fpc frames)
@@ -315,9 +316,9 @@ def main():
             returns (max-over-ranks seconds, last frames). Frame path with fpc > 1: `steps` frames
             as calls of fpc frames (the last call the remainder); self.total = frames timed."""
             calls = [self.fpc] * (steps // self.fpc) + ([steps % self.fpc] if steps % self.fpc else []) \
-                if (self.single and self.fpc > 1) else [1] * steps
+                if (self.single and self.fpc > 1) else [1] * (steps // self.kstep)
             self.total = sum(calls)
-            for i in range(warmup):
+            for i in range(warmup if self.single else max(1, warmup // self.kstep) if warmup else 0):
                 self.step(i, self.fpc)
             self.drain()
             torch.cuda.synchronize(dev)
@@ -339,7 +340,14 @@ def main():
                 all_reduce(el, dist.ReduceOp.MAX)
             return float(el.item()), frames
 
-    main_run = Runner(world if args.mode == "weak" else 1, frame_path=world == 1 and rtcomm is None)
+    # N > 1, weak scaling: a render call covers --frames-per-call steps (each rank's share of that many
+    # steps' N frames in one launch, one gather, one un-permute), as the one-GPU line renders that many
+    # frames per call; the step count must be a whole number of calls, else one step per call
+    kstep = 1
+    if world > 1 and args.mode == "weak" and rtcomm is None and args.frames_per_call > 1 and args.steps % args.frames_per_call == 0:
+        kstep = min(args.frames_per_call, 8)
+    main_run = Runner(world * kstep if args.mode == "weak" else 1, frame_path=world == 1 and rtcomm is None)
+    main_run.kstep = kstep
     plan = main_run.plan
 
     # rays per step (deterministic): counted once, summed over ranks
@@ -347,8 +355,8 @@ def main():
     ct = torch.tensor([int(c) for c in counts], dtype=torch.float64, device=dev)
     if world > 1:
         all_reduce(ct)
-    rays_per_step = float(ct.sum().item())
-    rays_by_kind = [int(x) for x in ct.tolist()]
+    rays_per_step = float(ct.sum().item()) / kstep
+    rays_by_kind = [int(x) // kstep for x in ct.tolist()]
 
     # ---- calibration: the view's per-view launch trials (rt_scene_trials) run on pipeline 0, one
     # frame at a time, before any timed or warm-up frame: a new view's first ~20 launches include
@@ -558,7 +566,7 @@ def main():
         total_rays = rays_per_step * args.steps
         value = total_rays / elapsed / 1e6
         queries = ch_tests / max(nt, 1)
-        per_rank_steps = args.profile_steps * fpc   # frames in the profiled launches
+        per_rank_steps = args.profile_steps * (fpc if main_run.single else kstep)   # frames (of steps) in the profiled launches
         traffic = traffic_src = None
         if args.accel == "bvh" and chain_launches > 0:
             # The chain kernel (every step of every sample per lane, RT_TUNE_CHAIN_FROM 0). Roof:
@@ -632,7 +640,8 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": wl["desc"],
-                "frames_per_step": plan.frames,
+                "frames_per_step": plan.frames // kstep,
+                "steps_per_call": kstep if world > 1 else None,
                 "width": WIDTH, "height": HEIGHT, "pf": PF, "max_lvl": MAX_LVL, "lights": [list(l) for l in LIGHTS],
                 "triangles": nt, "vertices": nv, "tile": TILE,
                 "parallelism": f"tile-shard{world}",

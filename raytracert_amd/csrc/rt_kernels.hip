@@ -2653,6 +2653,37 @@ __global__ __launch_bounds__(kBlock) void k_assemble_tiles(const uint8_t *__rest
     for (; k < n; ++k) dst[k] = src[k];
 }
 
+// The same un-permute with one thread per 16-B piece of a gathered tile row and the index math in 32
+// bits through the host's multiply-high divisors (launch_assemble_tiles takes it when every piece
+// index fits 32 bits): three times the threads of the per-row form and no 64-bit divisions. C4 at
+// 8 ranks: 8 frames in 0.0555 ms with the per-row form (1.8 TB/s of reads + writes).
+struct AssembleDivs { UDiv ppr, th, nslots, tiles_total, tiles_x; };
+__global__ __launch_bounds__(kBlock) void k_assemble_pieces(const uint8_t *__restrict__ gathered, int32_t width, int32_t height,
+                                                            int32_t tw, int32_t th, int32_t tiles_x, int32_t tiles_total,
+                                                            int32_t nranks, uint32_t slot0, uint32_t nslots, int32_t frames,
+                                                            uint32_t npieces, AssembleDivs dv, uint8_t *__restrict__ out) {
+    const uint32_t i = blockIdx.x * static_cast<uint32_t>(kBlock) + threadIdx.x;
+    if (i >= npieces) return;
+    const uint32_t row = udiv(i, dv.ppr), piece = i - row * dv.ppr.d;
+    const uint32_t tile = udiv(row, dv.th), r = row - tile * static_cast<uint32_t>(th);   // gathered tile (rank-major), its row
+    const uint32_t rank = udiv(tile, dv.nslots), slot = slot0 + (tile - rank * nslots);
+    const uint32_t g = slot * static_cast<uint32_t>(nranks) + rank;   // < 2^30 (rt_render_tiles_device's bound)
+    if (g >= static_cast<uint32_t>(frames) * static_cast<uint32_t>(tiles_total)) return;   // a padding slot
+    const uint32_t f = udiv(g, dv.tiles_total), t = g - f * static_cast<uint32_t>(tiles_total);
+    const uint32_t ty = udiv(t, dv.tiles_x), tx = t - ty * static_cast<uint32_t>(tiles_x);
+    const int y = static_cast<int>(ty) * th + static_cast<int>(r), x0 = static_cast<int>(tx) * tw;
+    if (y >= height) return;
+    const int n = min(tw, width - x0) * 3, k = static_cast<int>(piece) * 16;
+    if (k >= n) return;
+    const uint8_t *src = gathered + (static_cast<int64_t>(tile) * tw * th + static_cast<int64_t>(r) * tw) * 3 + k;
+    uint8_t *dst = out + ((static_cast<int64_t>(f) * height + y) * width + x0) * 3 + k;
+    if (k + 16 <= n && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0) {
+        *reinterpret_cast<uint4 *>(dst) = *reinterpret_cast<const uint4 *>(src);
+    } else {
+        for (int b = 0; b < 16 && k + b < n; ++b) dst[b] = src[b];
+    }
+}
+
 inline unsigned grid_for(int64_t n) { return static_cast<unsigned>((n + kBlock - 1) / kBlock); }
 
 }  // namespace
@@ -3023,6 +3054,16 @@ void launch_assemble_tiles(const uint8_t *gathered, int32_t width, int32_t heigh
     if (nslots < 0) nslots = slots - slot0;   // (default: the whole shard)
     const int64_t rows = static_cast<int64_t>(nranks) * nslots * th;   // one thread per gathered tile row
     if (rows <= 0 || static_cast<int64_t>(frames) * width * height <= 0) return;
+    const int64_t ppr = (static_cast<int64_t>(tw) * 3 + 15) / 16, npieces = rows * ppr;
+    if (npieces < (int64_t(1) << 32) - kBlock && slot0 + nslots < (int64_t(1) << 32)) {
+        const AssembleDivs dv{make_udiv(static_cast<uint32_t>(ppr)), make_udiv(static_cast<uint32_t>(th)),
+                              make_udiv(static_cast<uint32_t>(nslots)), make_udiv(static_cast<uint32_t>(tiles_total)),
+                              make_udiv(static_cast<uint32_t>(tiles_x))};
+        hipLaunchKernelGGL(k_assemble_pieces, dim3(static_cast<unsigned>((npieces + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                           gathered, width, height, tw, th, tiles_x, tiles_total, nranks, static_cast<uint32_t>(slot0),
+                           static_cast<uint32_t>(nslots), frames, static_cast<uint32_t>(npieces), dv, out);
+        return;
+    }
     hipLaunchKernelGGL(k_assemble_tiles, dim3(static_cast<unsigned>((rows + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
                        gathered, width, height, tw, th, tiles_x, tiles_total, nranks, slot0, nslots, frames, out);
 }

@@ -178,3 +178,20 @@ def test_bench_multi_rank_rehearsal(tmp_path, gpu_available):
     assert d["n_gpus"] == 2 and d["config"]["frames_per_step"] == 2
     assert d["rehearsal"]["frames_checked"] == 2 and d["rehearsal"]["all_equal_one_gpu_frame"]
     assert d["config"]["rays_per_step"] == 2 * 494405 and "strong" in d
+
+
+def test_bench_multi_rank_rehearsal_steps_per_call(tmp_path, gpu_available):
+    """The N>1 weak step with --frames-per-call 4: each rank renders its share of 4 steps' frames in one
+    call, one gather, one un-permute of 8 frames; rays and frames are still reported per step."""
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", "29534", os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "8",
+           "--warmup", "4", "--frames-per-call", "4", "--rehearse", "--workload", "c2", "--no-cpu", "--no-bf-roofline",
+           "--no-cold", "--no-path-compare"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["config"]["frames_per_step"] == 2 and d["config"]["steps_per_call"] == 4
+    assert d["rehearsal"]["frames_checked"] == 8 and d["rehearsal"]["all_equal_one_gpu_frame"]
+    assert d["config"]["rays_per_step"] == 2 * 494405
