@@ -1674,27 +1674,6 @@ __device__ __forceinline__ void offset_point(V3 &point, V3 dest) {   // addOffse
 #ifndef RT_HOIST_LNORM
 #define RT_HOIST_LNORM 1   // diffuse's normalize(light position) from ShadeParams::lnorm (made on the host)
 #endif
-#ifndef RT_SPEC_SKIP
-#define RT_SPEC_SKIP 1     // skip the exact specular powf where its term cannot change the colour (spec_negligible)
-#endif
-// The specular term t_k = (Ks_k * powf(st, Ns)) * Tr (:225-228, :353) added to colour component c_k
-// leaves c_k's bits unchanged when 0 <= t_k < ulp(c_k) / 2 (round to nearest keeps c_k), and
-// ulp(c) / 2 > c * 2^-25 for normal c. An upper bound of powf from the hardware log2/exp2 (v_log_f32,
-// v_exp_f32: ~1 ulp each), with the exponent raised by 0.1% + 0.01 and the result by 1% (far more
-// than their error), decides that without the exact double-precision powf: true when, for every
-// component, Ks_k == 0 (t_k = 0 * p = 0, p finite: st < 1, Ns > 0), or c_k >= 2^-60 and
-// Ks_k * P_ub * |Tr| < c_k * 2^-26 (rounding of that product and of t_k's two products stays below
-// the factor 2 of margin; an underflowed bound still leaves t_k <= Ks_k |Tr| 2^-126 < c_k 2^-25 for
-// Ks_k, |Tr| < 2^20). NaN anywhere fails a comparison and takes the exact path. Highlights (st near 1)
-// take the exact path; elsewhere, at Ns ~ 96, the term is below the colour's resolution.
-__device__ __forceinline__ bool spec_negligible(float st, float Ns, V3 Ks, float Tr, V3 c) {
-    if (!(st >= 0.0f && st < 1.0f && Ns > 0.0f && fabsf(Tr) < 0x1p20f)) return false;
-    const float E = Ns * __builtin_amdgcn_logf(st);   // <= 0; -inf for st = 0
-    const float lim = __builtin_amdgcn_exp2f(E * 0.999f + 0.01f) * 1.01f * fabsf(Tr);
-    auto ok = [&](float ks, float ck) { return ks == 0.0f || (ks < 0x1p20f && ck >= 0x1p-60f && ks * lim < ck * 0x1p-26f); };
-    return ok(Ks.x, c.x) && ok(Ks.y, c.y) && ok(Ks.z, c.z);
-}
-
 #ifndef RT_NORMAL_TABLE
 #define RT_NORMAL_TABLE 0  // the hit normal's normalize() states from DevScene::ntab (k_normal_table). Measured
                            // (multi-frame launches): C5 (4 lights) 6.594 -> 6.566 ms, C4 (2 lights) 0.3400 ->
@@ -1762,13 +1741,9 @@ __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadePa
             V3 H = add(Vv, Lv);
             normalize(H);
             float st = max_std(dot(H, normal), 0.0f);
-            // (a term below half an ulp of every colour component it is added to leaves the colour's bits
-            // as they are: then the exact powf is not needed, spec_negligible)
-            if (!RT_SPEC_SKIP || !spec_negligible(st, m.Ns, Ks, m.Tr, color)) {
-                st = spec_powf(st, m.Ns);
-                spec = add(spec, scale(Ks, st));
-                color = add(color, scale(spec, m.Tr));               // :353
-            }
+            st = spec_powf(st, m.Ns);
+            spec = add(spec, scale(Ks, st));
+            color = add(color, scale(spec, m.Tr));                   // :353
         }
     }
     if ((f & RT_REFRACTION) && (m.Tr < 1) && lvl < p.max_lvl) {     // :357-359 -> refraction :290-330
