@@ -147,3 +147,24 @@ def test_workspace_layout_covers_every_array(cap, steps, lights):
         assert size >= n
         end = off + size
     assert end <= total
+
+
+def test_multiframe_and_reserve_entries_refuse_without_a_device(tmp_path):
+    """rt_render_frames_device and rt_scene_reserve (r05) on a host-only scene return RT_E_NODEV, and
+    with a NULL scene RT_E_ARG, before touching HIP (no GPU needed)."""
+    p = tmp_path / "t.obj"
+    p.write_text("v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 3\n")
+    s = R.Scene.load(str(p), device=R.RT_HOST_ONLY)
+    rp = R.RenderParams(width=8, height=8, pf=1, max_lvl=1)
+    with pytest.raises(R.RtError) as ei:
+        s.reserve(rp, 16, 16)
+    assert ei.value.code == _capi.RT_E_NODEV
+    with pytest.raises(R.RtError) as ei:
+        s.render_frames_device([rp, rp], 16, 16, [1, 2], 8 * 8 * 3)
+    assert ei.value.code == _capi.RT_E_NODEV
+    lib = _capi.lib()
+    cp = rp.to_c()
+    outs = (C.c_void_p * 2)(1, 2)
+    assert lib.rt_render_frames_device(None, C.byref(cp), 2, 16, 16, outs, 192, None, None) == _capi.RT_E_ARG
+    assert lib.rt_scene_reserve(None, C.byref(cp), 16, 16, 0) == _capi.RT_E_ARG
+    assert _capi.MAX_FRAMES_PER_CALL == 8
