@@ -223,8 +223,7 @@ int rt_trace_frame_samples(rt_scene *scene, const rt_params *params, int32_t lay
  * on the scene's stream. */
 int rt_scene_reserve(rt_scene *scene, const rt_params *params, int32_t tile_w, int32_t tile_h, int32_t samples_layout);
 /* Page-locked host memory (hipHostMalloc on the scene's device's runtime), for rt_trace_frame_samples'
- * output and other large device-to-host results; zero-filled by the device at allocation, which maps it
- * for the GPU there rather than in the first copy into it. */
+ * output and other large device-to-host results. */
 int  rt_host_alloc(size_t bytes, void **out);
 void rt_host_free(void *ptr);
 /* The whole frame, row-major (height x width x 3 bytes, the PPM's pixel order), into the DEVICE
