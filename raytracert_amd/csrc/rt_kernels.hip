@@ -2361,15 +2361,11 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
                 const int rk = __popcll((live ? lm : ~lm) & below);   // rank among the live (dead) lanes
                 const bool paired = rk < npair;
                 // lane k (< npair) receives pair k's owner and helper lane ids (the others write to lane 63,
-                // which no pair reads: npair <= 32), and each pair member reads its partner's from lane k.
-                // (All 64 lanes run the permutes: a permute reads nothing from a lane masked off, so reading
-                // lane k under a pair member's branch would return 0 whenever lane k is not one.)
+                // which no pair reads: npair <= 32), and each pair member reads its partner's from lane k
                 const int at_owner = __builtin_amdgcn_ds_permute(4 * ((live && paired) ? rk : kWave - 1), lane);
                 const int at_helper = __builtin_amdgcn_ds_permute(4 * ((!live && paired) ? rk : kWave - 1), lane);
-                const int o_at = __builtin_amdgcn_ds_bpermute(4 * rk, at_owner);
-                const int h_at = __builtin_amdgcn_ds_bpermute(4 * rk, at_helper);
-                const int dsrc = (!live && paired) ? o_at : lane;
-                const int dh = (live && paired) ? h_at : lane;
+                const int dsrc = (!live && paired) ? __builtin_amdgcn_ds_bpermute(4 * rk, at_owner) : lane;
+                const int dh = (live && paired) ? __builtin_amdgcn_ds_bpermute(4 * rk, at_helper) : lane;
                 if (!live && !paired) continue;
                 if (live && step > first) atomicAdd(&s_q[step], 1);
                 const Secondary sec = chain_step<kAnyHit, W, kCount, kInLane, kSteal>(
