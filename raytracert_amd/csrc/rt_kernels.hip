@@ -1674,9 +1674,6 @@ __device__ __forceinline__ void offset_point(V3 &point, V3 dest) {   // addOffse
 #ifndef RT_HOIST_LNORM
 #define RT_HOIST_LNORM 1   // diffuse's normalize(light position) from ShadeParams::lnorm (made on the host)
 #endif
-#ifndef RT_DEAD_HELPERS
-#define RT_DEAD_HELPERS 1  // dead-lane shadow helpers in whole waves of the fused chain launch (k_chain)
-#endif
 #ifndef RT_NORMAL_TABLE
 #define RT_NORMAL_TABLE 0  // the hit normal's normalize() states from DevScene::ntab (k_normal_table). Measured
                            // (multi-frame launches): C5 (4 lights) 6.594 -> 6.566 ms, C4 (2 lights) 0.3400 ->
@@ -1944,9 +1941,7 @@ template <bool kAnyHit, int W, bool kCount, bool kInLane = false, bool kSteal = 
 __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeParams &p, const DevWork &w, int step,
                                                 int sample, V3 org, V3 dst, int lvl, const LaneStack &stack, int *s_sh,
                                                 WorkTally<kCount> &wc, WorkTally<kCount> &ws, int role = 0, int roles = 1,
-                                                int plen = kWave, Park park = Park{nullptr}, int dsrc = -1, int dh = -1) {
-    // (dsrc >= 0: dead-lane pairing, RT_DEAD_HELPERS: this lane's owner is lane dsrc (itself for an
-    // owner), an owner's helper is lane dh (itself when unpaired), roles = 2 for a pair, else 1)
+                                                int plen = kWave, Park park = Park{nullptr}) {
     Secondary none;
     none.state = kChildNone;
     none.local = mk(0, 0, 0);   // trace() miss: black (:389-391)
@@ -1960,8 +1955,8 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
     bvh_query_w<false, W, kSteal>(sc, org, ray, role == 0, bidx, bI, stack, wc.tests, wc.visits);
     if (bidx >= sc.nt) { w.counters[kErrorSlot] = 1; bidx = -1; }
     const int lane = __lane_id();
-    if (roles > 1 || dsrc >= 0) {   // helpers take their owner's hit (owner and helpers are all active here)
-        const int src = dsrc >= 0 ? dsrc : role ? lane - role * plen : lane;
+    if (roles > 1) {   // helpers take their owner's hit (owner and helpers are all active here)
+        const int src = role ? lane - role * plen : lane;
         bidx = __shfl(bidx, src);
         bI = mk(__shfl(bI.x, src), __shfl(bI.y, src), __shfl(bI.z, src));
     }
@@ -1982,14 +1977,9 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
             bvh_query_w<kAnyHit, W, kSteal>(sc, so, sd, true, sidx, sI, stack, ws.tests, ws.visits);
             if (sidx >= 0 && !sc.mats[sc.tri_mat[sidx]].transparent) mask |= 1u << l;   // :253-257
         }
-        if (dsrc >= 0) {   // the pair's helper's verdicts (an unpaired owner reads its own)
-            const uint32_t m = static_cast<uint32_t>(__shfl(static_cast<int>(mask), dh));
+        for (int r = 1; r < roles; ++r) {   // the helpers' verdicts (all lanes of the group active again)
+            const uint32_t m = static_cast<uint32_t>(__shfl(static_cast<int>(mask), min(lane + r * plen, kWave - 1)));
             if (role == 0) mask |= m;
-        } else {
-            for (int r = 1; r < roles; ++r) {   // the helpers' verdicts (all lanes of the group active again)
-                const uint32_t m = static_cast<uint32_t>(__shfl(static_cast<int>(mask), min(lane + r * plen, kWave - 1)));
-                if (role == 0) mask |= m;
-            }
         }
     }
     if (role != 0) return none;   // (a helper's return value is not used)
@@ -2310,11 +2300,6 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         const int roles = (kInLane && !kSteal && nparts > 1 && scb.shadow_helpers && (pl.flags & RT_SHADOWS))
                               ? max(1, min(kWave / plen, pl.n_lights)) : 1;
         const int role = (roles > 1 && lane >= plen && lane < roles * plen) ? lane / plen : 0;
-        // dead-lane shadow helpers (RT_DEAD_HELPERS): in a whole wave, at every chain step the lanes with no
-        // live chain (ended, or no sample) pair with live ones in lane order and walk every other light's
-        // shadow ray of their owner's hit, so a pair's lights are walked side by side
-        const bool dyn = RT_DEAD_HELPERS && kInLane && !kSteal && roles == 1 && scb.shadow_helpers &&
-                         (pl.flags & RT_SHADOWS) && pl.n_lights > 1;
         [&]() {
         bool own = lane_on && j < nq;
         V3 org = mk(0, 0, 0), dst = mk(0, 0, 0);
@@ -2331,10 +2316,9 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
                 const bool o = __shfl(static_cast<int>(own), role ? lane - role * plen : lane) != 0;
                 if (role) own = o;
             }
-            if (dyn && !(own && lane_on)) own = false;   // (stays in the wave's step loop as a possible helper)
-            else if (!own || (role == 0 && !lane_on)) return;
-            if (own && role == 0) px = gl.out_mode == 2 ? static_cast<int>(pxi) * fuse_spp + sub : static_cast<int>(pxi);
-            if (own && gl.out_mode == 2 && gl.sample_stride == 9 && role == 0) {   // the record's ray (RT_SAMPLES_RAY_RGB)
+            if (!own || (role == 0 && !lane_on)) return;
+            if (role == 0) px = gl.out_mode == 2 ? static_cast<int>(pxi) * fuse_spp + sub : static_cast<int>(pxi);
+            if (gl.out_mode == 2 && gl.sample_stride == 9 && role == 0) {   // the record's ray (RT_SAMPLES_RAY_RGB)
                 float *r = of32f() + 9 * static_cast<int64_t>(px);
                 r[0] = org.x; r[1] = org.y; r[2] = org.z; r[3] = dst.x; r[4] = dst.y; r[5] = dst.z;
             }
@@ -2350,39 +2334,6 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
             sample = as_int(qo.w);
             org = mk(qo.x, qo.y, qo.z);
             dst = mk(qd.x, qd.y, qd.z);
-        }
-        if (dyn) {
-            bool live = own;
-            const unsigned long long below = (1ull << lane) - 1ull;
-            for (int step = first; step < kChainSteps; ++step) {
-                const unsigned long long lm = __ballot(live);
-                if (lm == 0) break;
-                const int nlive = __popcll(lm), npair = min(nlive, kWave - nlive);
-                const int rk = __popcll((live ? lm : ~lm) & below);   // rank among the live (dead) lanes
-                const bool paired = rk < npair;
-                // lane k (< npair) receives pair k's owner and helper lane ids (the others write to lane 63,
-                // which no pair reads: npair <= 32), and each pair member reads its partner's from lane k
-                const int at_owner = __builtin_amdgcn_ds_permute(4 * ((live && paired) ? rk : kWave - 1), lane);
-                const int at_helper = __builtin_amdgcn_ds_permute(4 * ((!live && paired) ? rk : kWave - 1), lane);
-                const int dsrc = (!live && paired) ? __builtin_amdgcn_ds_bpermute(4 * rk, at_owner) : lane;
-                const int dh = (live && paired) ? __builtin_amdgcn_ds_bpermute(4 * rk, at_helper) : lane;
-                if (!live && !paired) continue;
-                if (live && step > first) atomicAdd(&s_q[step], 1);
-                const Secondary sec = chain_step<kAnyHit, W, kCount, kInLane, kSteal>(
-                    scb, pl, wb, step, sample, org, dst, lvl, stack, s_sh, wc, ws, live ? 0 : 1, paired ? 2 : 1, plen, park,
-                    dsrc, dh);
-                if (!live) continue;
-                if (sec.state != kChildTrace) {   // the chain ends here: fold it in the lane (fold_chain's arithmetic)
-                    rgb = fold_inlane(scb, wb, first, step, sample,
-                                      sec.state == kChildZero ? add(sec.local, mk(0.0f, 0.0f, 0.0f)) : sec.local);
-                    live = false;
-                    continue;
-                }
-                org = sec.org;
-                dst = sec.dst;
-                lvl = sec.lvl;
-            }
-            return;
         }
         for (int step = first; step < kChainSteps; ++step) {
             if (step > first && role == 0) atomicAdd(&s_q[step], 1);
