@@ -1901,6 +1901,9 @@ __device__ __forceinline__ void store_pixel(V3 rgb, int64_t o, uint8_t *__restri
 }
 
 constexpr int kChainSteps = 256;   // max_lvl <= 254
+#ifndef RT_MULTI_WPE
+#define RT_MULTI_WPE RT_CHAIN_WPE   // the multi-frame instantiation's (A/B: its launches are VALU-bound)
+#endif
 #ifndef RT_CHAIN_WPE
 #define RT_CHAIN_WPE 5   // r02, with in-lane chains: 5 (0.493-0.499 ms) vs 6 (0.533, more spills) vs 4 (0.51);
                          // r01, before them: 6 (80 VGPRs, 36 B spill) beat 5 (92, none) and 7
@@ -2171,7 +2174,7 @@ __device__ __forceinline__ uint32_t chain_kernarg_mismatch(int first, int ordere
     return bad;
 }
 template <int W, bool kAnyHit, bool kCount, bool kInLane = false, bool kSteal = false, bool kQuad = false, bool kMulti = false>
-__global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kSteal ? RT_STEAL_WPE : RT_CHAIN_WPE))) void k_chain(
+__global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kSteal ? RT_STEAL_WPE : kMulti ? RT_MULTI_WPE : RT_CHAIN_WPE))) void k_chain(
     const DevScene sc, const ShadeParams p, DevWork w, int first, int ordered, uint8_t *__restrict__ out_u8,
     float *__restrict__ out_f32, int fuse_spp, int spb, int nbatch, const FrameGeom g, int split, int split8, const FrameSet fs) {
     extern __shared__ int32_t lds_stack[];
