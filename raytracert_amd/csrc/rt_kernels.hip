@@ -2917,7 +2917,8 @@ void launch_chain(const DevScene &s0, const DevWork &w, const ShadeParams &p, in
     const int split = s2 | (s4 << 16);
     const FrameGeom geom = g ? with_divisors(*g) : FrameGeom{};
     // distribution 4 (dynamic wave tasks): a resident grid, each wave takes tasks until none remain
-    const int grid_cap = (fused && s.chain_split == 4) ? std::max(1, std::min(s.bvh_grid, s.resident_grid)) : s.bvh_grid;
+    const int resident = multi ? s.resident_grid * RT_MULTI_WPE / RT_CHAIN_WPE : s.resident_grid;   // (its own waves per EU)
+    const int grid_cap = (fused && s.chain_split == 4) ? std::max(1, std::min(s.bvh_grid, resident)) : s.bvh_grid;
     FrameSet frames{};
     frames.count = 1;
     if (multi) frames = *fs;
