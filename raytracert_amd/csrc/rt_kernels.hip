@@ -1943,8 +1943,16 @@ struct Park {
 template <bool kAnyHit, int W, bool kCount, bool kInLane = false, bool kSteal = false>
 __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeParams &p, const DevWork &w, int step,
                                                 int sample, V3 org, V3 dst, int lvl, const LaneStack &stack, int *s_sh,
-                                                WorkTally<kCount> &wc, WorkTally<kCount> &ws, int role = 0, int roles = 1,
-                                                int plen = kWave, Park park = Park{nullptr}) {
+                                                WorkTally<kCount> &wc, WorkTally<kCount> &ws, bool live = true,
+                                                bool pair = false, Park park = Park{nullptr}) {
+    // kPair (the fused in-lane launch): every lane of the wave calls this at every step of its batch,
+    // live or not (live: this lane's chain traces a ray at this step); with `pair`, once the closest
+    // hits are known the lanes without a hit (chain ended, missed, or no sample) help the lanes with
+    // one walk their shadow rays: with nh hit lanes and nd = 64 - nh others, each hit lane gets
+    // G = min(L - 1, nd / nh) helpers (the same G for all, so the shadow phase is uniform), the group
+    // walking lights role, role + G + 1, ... Each (hit, light) verdict is still one walk of the same
+    // ray, so the mask, and every colour, is the one the owner alone would have made.
+    constexpr bool kPair = kInLane && !kSteal;
     Secondary none;
     none.state = kChildNone;
     none.local = mk(0, 0, 0);   // trace() miss: black (:389-391)
@@ -1955,37 +1963,56 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
         park.put(0, ray.x); park.put(1, ray.y); park.put(2, ray.z);
         park.put(3, as_float(lvl)); park.put(4, as_float(sample));
     }
-    bvh_query_w<false, W, kSteal>(sc, org, ray, role == 0, bidx, bI, stack, wc.tests, wc.visits);
+    bvh_query_w<false, W, kSteal>(sc, org, ray, live, bidx, bI, stack, wc.tests, wc.visits);
     if (bidx >= sc.nt) { w.counters[kErrorSlot] = 1; bidx = -1; }
-    const int lane = __lane_id();
-    if (roles > 1) {   // helpers take their owner's hit (owner and helpers are all active here)
-        const int src = role ? lane - role * plen : lane;
-        bidx = __shfl(bidx, src);
-        bI = mk(__shfl(bI.x, src), __shfl(bI.y, src), __shfl(bI.z, src));
-    }
-    if (bidx < 0) {
-        if (!kInLane) shade_miss(w, step, sample);
+    const bool hit = live && bidx >= 0;
+    if (!kPair && !hit) {
+        if (!kInLane && live) shade_miss(w, step, sample);
         return none;
     }
     uint32_t mask = 0;   // isShadow per light (:241-261)
     const bool shadows = (p.flags & RT_SHADOWS) && p.n_lights > 0;
     if (shadows) {
-        if (role == 0) atomicAdd(&s_sh[step], p.n_lights);
-        const V3 so = mk(bI.x + 0.1f, bI.y + 0.1f, bI.z + 0.1f);                // :248
-        for (int l = role; l < p.n_lights; l += roles) {
-            int sidx = -1;
-            V3 sI = mk(0, 0, 0);
-            const V3 Lp = light_at<false>(p.lights, p.light_ext, l);   // (the chain launch: <= RT_MAX_LIGHTS)
-            const V3 sd = mk(Lp.x - so.x, Lp.y - so.y, Lp.z - so.z);
-            bvh_query_w<kAnyHit, W, kSteal>(sc, so, sd, true, sidx, sI, stack, ws.tests, ws.visits);
-            if (sidx >= 0 && !sc.mats[sc.tri_mat[sidx]].transparent) mask |= 1u << l;   // :253-257
+        const int lane = __lane_id();
+        int role = 0, G = 0, nh = 0, rk = 0, at_helper = 0;
+        if (kPair && pair) {
+            const unsigned long long hm = __ballot(hit);
+            nh = __popcll(hm);
+            G = nh ? min(p.n_lights - 1, (kWave - nh) / nh) : 0;   // (wave-uniform)
+            if (G > 0) {
+                rk = __popcll((hit ? hm : ~hm) & ((1ull << lane) - 1ull));   // rank among the hit (other) lanes
+                // lane k receives the hit lane of rank k and the other lane of rank k (lane 63 takes the
+                // unused writes: with G > 0 fewer than 64 lanes are of either kind); every lane runs the
+                // permutes, which read nothing from a masked lane
+                const int at_owner = __builtin_amdgcn_ds_permute(4 * (hit ? rk : kWave - 1), lane);
+                at_helper = __builtin_amdgcn_ds_permute(4 * (hit ? kWave - 1 : rk), lane);
+                const int owner = __builtin_amdgcn_ds_bpermute(4 * (rk % nh), at_owner);
+                const bool helps = !hit && rk < G * nh;
+                if (helps) role = 1 + rk / nh;
+                const int src = helps ? owner : lane;   // helpers take their owner's hit
+                bidx = __shfl(bidx, src);
+                bI = mk(__shfl(bI.x, src), __shfl(bI.y, src), __shfl(bI.z, src));
+            }
         }
-        for (int r = 1; r < roles; ++r) {   // the helpers' verdicts (all lanes of the group active again)
-            const uint32_t m = static_cast<uint32_t>(__shfl(static_cast<int>(mask), min(lane + r * plen, kWave - 1)));
-            if (role == 0) mask |= m;
+        if (hit || role > 0) {
+            if (role == 0) atomicAdd(&s_sh[step], p.n_lights);
+            const V3 so = mk(bI.x + 0.1f, bI.y + 0.1f, bI.z + 0.1f);                // :248
+            for (int l = role; l < p.n_lights; l += G + 1) {
+                int sidx = -1;
+                V3 sI = mk(0, 0, 0);
+                const V3 Lp = light_at<false>(p.lights, p.light_ext, l);   // (the chain launch: <= RT_MAX_LIGHTS)
+                const V3 sd = mk(Lp.x - so.x, Lp.y - so.y, Lp.z - so.z);
+                bvh_query_w<kAnyHit, W, kSteal>(sc, so, sd, true, sidx, sI, stack, ws.tests, ws.visits);
+                if (sidx >= 0 && !sc.mats[sc.tri_mat[sidx]].transparent) mask |= 1u << l;   // :253-257
+            }
+        }
+        for (int r = 0; r < G; ++r) {   // an owner's helpers' verdicts (ranks rk, rk + nh, ... among the others)
+            const int hl = __builtin_amdgcn_ds_bpermute(4 * min(rk + r * nh, kWave - 1), at_helper);
+            const uint32_t m = static_cast<uint32_t>(__shfl(static_cast<int>(mask), hl));
+            if (hit) mask |= m;
         }
     }
-    if (role != 0) return none;   // (a helper's return value is not used)
+    if (!hit) return none;   // (a helper's or an idle lane's return value is not used)
     if (RT_LDS_PARK && park.base) {
         ray = mk(park.get(0), park.get(1), park.get(2));
         lvl = as_int(park.get(3));
@@ -2289,8 +2316,9 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         V3 rgb = mk(0, 0, 0);   // fused pixels: this lane's folded chain and its pixel (valid samples)
         int px = -1;   // (out_mode 2: the sample's output slot, pixel x spp + sub-sample)
-        // shadow helpers (RT_TUNE_SHADOW_HELPERS): in a split wave of the fused launch the lanes past
-        // the part's plen samples help their owners' shadow walks, roles = lanes per sample (<= lights)
+        // shadow helpers (RT_TUNE_SHADOW_HELPERS): at every step the lanes without a closest hit (a split
+        // wave's lanes past the part's samples, chains that ended or missed) walk shadow rays for the
+        // lanes with one (chain_step's kPair)
         // the quad walk (RT_TUNE_QUAD_WALK): a quarter-tier part's samples on four lanes each
         // (its own instantiation, kQuad: compiled into the default kernel the quad path's registers moved the
         // per-lane path's allocation from 24 to 92 B of spill per lane)
@@ -2300,9 +2328,8 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
                 quad_batch<kAnyHit, kCount>(scb, pl, wb, gl, nfr > 1 ? fcs : gl.corners, lds_stack, s_q, s_sh, wc, ws, o8f(), of32f(),
                                             fuse_spp, pb * spb + part * plen, min(plen, spb - part * plen), nq);
         } else {
-        const int roles = (kInLane && !kSteal && nparts > 1 && scb.shadow_helpers && (pl.flags & RT_SHADOWS))
-                              ? max(1, min(kWave / plen, pl.n_lights)) : 1;
-        const int role = (roles > 1 && lane >= plen && lane < roles * plen) ? lane / plen : 0;
+        constexpr bool kPair = kInLane && !kSteal;   // (every lane stays in the step loop, chain_step)
+        const bool pair = kPair && scb.shadow_helpers && (pl.flags & RT_SHADOWS) && pl.n_lights > 1;
         [&]() {
         bool own = lane_on && j < nq;
         V3 org = mk(0, 0, 0), dst = mk(0, 0, 0);
@@ -2315,13 +2342,10 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
                 if (gl.out_mode == 0 && o8 && sub == 0) { o8[3 * pxi] = 0; o8[3 * pxi + 1] = 0; o8[3 * pxi + 2] = 0; }
                 own = false;
             }
-            if (roles > 1) {   // a helper follows its owner's sample (all lanes are still here)
-                const bool o = __shfl(static_cast<int>(own), role ? lane - role * plen : lane) != 0;
-                if (role) own = o;
-            }
-            if (!own || (role == 0 && !lane_on)) return;
-            if (role == 0) px = gl.out_mode == 2 ? static_cast<int>(pxi) * fuse_spp + sub : static_cast<int>(pxi);
-            if (gl.out_mode == 2 && gl.sample_stride == 9 && role == 0) {   // the record's ray (RT_SAMPLES_RAY_RGB)
+            own = own && lane_on;
+            if (!kPair && !own) return;
+            if (own) px = gl.out_mode == 2 ? static_cast<int>(pxi) * fuse_spp + sub : static_cast<int>(pxi);
+            if (own && gl.out_mode == 2 && gl.sample_stride == 9) {   // the record's ray (RT_SAMPLES_RAY_RGB)
                 float *r = of32f() + 9 * static_cast<int64_t>(px);
                 r[0] = org.x; r[1] = org.y; r[2] = org.z; r[3] = dst.x; r[4] = dst.y; r[5] = dst.z;
             }
@@ -2338,21 +2362,20 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
             org = mk(qo.x, qo.y, qo.z);
             dst = mk(qd.x, qd.y, qd.z);
         }
+        bool live = own;   // (kPair: lanes stay after their chain ends, as helpers; the loop ends with the wave's last chain)
         for (int step = first; step < kChainSteps; ++step) {
-            if (step > first && role == 0) atomicAdd(&s_q[step], 1);
+            if (kPair && !__any(live)) break;
+            if (live && step > first) atomicAdd(&s_q[step], 1);
             const Secondary sec = chain_step<kAnyHit, W, kCount, kInLane, kSteal>(scb, pl, wb, step, sample, org, dst, lvl, stack,
-                                                                                  s_sh, wc, ws, role, roles, plen, park);
-            bool cont = sec.state == kChildTrace;
-            if (roles > 1) cont = __shfl(static_cast<int>(cont), role ? lane - role * plen : lane) != 0;   // the owner's
-            if (role) {
-                if (!cont) break;
-                continue;
-            }
+                                                                                  s_sh, wc, ws, live, pair, park);
+            if (!live) continue;
             if (sec.state != kChildTrace) {
                 if (kInLane)   // the chain ends here: fold it in the lane (fold_chain's arithmetic)
                     rgb = fold_inlane(scb, wb, first, step, sample,
                                       sec.state == kChildZero ? add(sec.local, mk(0.0f, 0.0f, 0.0f)) : sec.local);
-                break;
+                live = false;
+                if (!kPair) break;
+                continue;
             }
             org = sec.org;
             dst = sec.dst;
