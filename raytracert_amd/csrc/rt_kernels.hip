@@ -1674,6 +1674,9 @@ __device__ __forceinline__ void offset_point(V3 &point, V3 dest) {   // addOffse
 #ifndef RT_HOIST_LNORM
 #define RT_HOIST_LNORM 1   // diffuse's normalize(light position) from ShadeParams::lnorm (made on the host)
 #endif
+#ifndef RT_PAIR_CLOSEST
+#define RT_PAIR_CLOSEST 1  // paired shadow helpers also in the closest-hit-shadow instantiations (scenes with transparency)
+#endif
 #ifndef RT_NORMAL_TABLE
 #define RT_NORMAL_TABLE 0  // the hit normal's normalize() states from DevScene::ntab (k_normal_table). Measured
                            // (multi-frame launches): C5 (4 lights) 6.594 -> 6.566 ms, C4 (2 lights) 0.3400 ->
@@ -1952,7 +1955,7 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
     // G = min(L - 1, nd / nh) helpers (the same G for all, so the shadow phase is uniform), the group
     // walking lights role, role + G + 1, ... Each (hit, light) verdict is still one walk of the same
     // ray, so the mask, and every colour, is the one the owner alone would have made.
-    constexpr bool kPair = kInLane && !kSteal;
+    constexpr bool kPair = kInLane && !kSteal && (kAnyHit || RT_PAIR_CLOSEST);
     Secondary none;
     none.state = kChildNone;
     none.local = mk(0, 0, 0);   // trace() miss: black (:389-391)
@@ -2328,7 +2331,7 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
                 quad_batch<kAnyHit, kCount>(scb, pl, wb, gl, nfr > 1 ? fcs : gl.corners, lds_stack, s_q, s_sh, wc, ws, o8f(), of32f(),
                                             fuse_spp, pb * spb + part * plen, min(plen, spb - part * plen), nq);
         } else {
-        constexpr bool kPair = kInLane && !kSteal;   // (every lane stays in the step loop, chain_step)
+        constexpr bool kPair = kInLane && !kSteal && (kAnyHit || RT_PAIR_CLOSEST);   // (every lane stays in the step loop, chain_step)
         const bool pair = kPair && scb.shadow_helpers && (pl.flags & RT_SHADOWS) && pl.n_lights > 1;
         [&]() {
         bool own = lane_on && j < nq;
