@@ -2,6 +2,7 @@
 // the render driver (rt_capi.cpp) and the kernels (rt_kernels.hip).
 #pragma once
 
+#include <cmath>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -54,6 +55,14 @@ struct alignas(16) TriRec {
     float n[3];  float D;
 };
 static_assert(sizeof(TriRec) == 64, "TriRec must be 64 bytes");
+// The device copy of a record when the kernels divide by the reciprocal slot (tri_rcp_records):
+// D replaced by RN(1/D) for normal |D| in [2^-30, 2^30], else NaN (those lanes divide by the
+// recomputed D). The host's own copy (BVH build, validation) keeps D.
+inline TriRec tri_rcp_slot(TriRec r) {
+    const float a = std::fabs(r.D);
+    r.D = (std::isnormal(r.D) && a >= 0x1p-30f && a <= 0x1p30f) ? 1.0f / r.D : NAN;
+    return r;
+}
 
 struct alignas(16) DevMaterial {
     float Kd[3]; float Ns;

@@ -202,6 +202,9 @@ void launch_intersect_only(const DevScene &s, const float4 *org, const float4 *d
                            int32_t *idx, float4 *I, hipStream_t stream);
 // calculateNormals on the device (face normal per triangle into normals[i].xyz)
 void launch_face_normals(const float *xyz, const uint32_t *tri_v, int32_t nt, float4 *normals, hipStream_t stream);
+// True when this build's test_triangle reads RN(1/D) from the records' D slot (RT_TRI_RCP): the
+// uploads then pass every record through tri_rcp_slot (rt_internal.h).
+bool tri_rcp_records();
 void launch_normal_table(float4 *normals, float4 *ntab, int32_t nt, hipStream_t stream);
 // Un-permute gathered tile shards ([nranks][slots][th][tw][3], tile g of the frames x T tiles in
 // rank g % nranks, slot g / nranks) into frames x height x width x 3 bytes; with slot0 / nslots, a

@@ -149,6 +149,22 @@ __device__ __forceinline__ void sgpr_fence(const TriRec &T) {
 // kStages (the brute-force roofline's counting pass only): stg[k] += 1 for each stage the test reaches
 // (kTestStageFlops: 0 the plane terms, 1 the division, 2 the in-plane coordinates and s, 3 t, 4 the
 // distance), so the work a launch performed is counted, not a union path every test is assumed to take.
+#ifndef RT_TRI_RCP
+#define RT_TRI_RCP 0   // 1: measured no faster (profiles/r05zi_ab_tri_rcp.txt)
+#endif
+// The s and t divisions by D (:144, :148) from the record's reciprocal slot (RT_TRI_RCP, r05): the
+// uploaded records carry rD = RN(1/D) in D's place (NaN where |D| is outside [2^-30, 2^30] or D is
+// not normal; tri_rcp_slot) and D is recomputed from uu, uv, vv as the loader computes it (:140, the
+// same bits). With q = RN(n rD) in [2^-30, 2^30] every intermediate is normal, the residual
+// fma(-q, D, n) is exact and q + r rD rounds to the correctly rounded n / D (Markstein's correction;
+// tools/markstein_gpu.hip checks all 2^46 significand pairs); elsewhere (rD NaN, n near 0 or huge)
+// the lane divides. Five instructions instead of ~11 for both divisions of a test that reaches them.
+__device__ __forceinline__ float div_by_rec(float n, float D, float rD) {
+    const float q = n * rD;
+    if (__builtin_expect(fabsf(q) >= 0x1p-30f && fabsf(q) <= 0x1p30f, 1)) return fmaf(fmaf(-q, D, n), rD, q);
+    return n / D;
+}
+
 constexpr int kTestStages = 5;
 constexpr int kTestStageFlops[kTestStages] = {14, 1, 23, 5, 9};
 template <bool kAnyHit, bool kLex = false, bool kSignFirst = false, bool kStages = false>
@@ -169,10 +185,19 @@ __device__ __forceinline__ void test_triangle(const TriRec &T, int t, V3 o, V3 d
     const V3 w = mk(I.x - T.t0[0], I.y - T.t0[1], I.z - T.t0[2]);               // :137
     const float wu = w.x * T.u[0] + w.y * T.u[1] + w.z * T.u[2];                 // :138
     const float wv = w.x * T.v[0] + w.y * T.v[1] + w.z * T.v[2];                 // :139
+#if RT_TRI_RCP
+    const float D = T.uv * T.uv - T.uu * T.vv;                                  // :140 (T.D holds rD)
+    const float s = div_by_rec(T.uv * wv - T.vv * wu, D, T.D);                  // :144
+#else
     const float s = (T.uv * wv - T.vv * wu) / T.D;                              // :144
+#endif
     if (s < 0 || s > 1) return;                                                 // :145
     if (kStages) ++stg[3];
+#if RT_TRI_RCP
+    const float tt = div_by_rec(T.uv * wu - T.uu * wv, D, T.D);                 // :148
+#else
     const float tt = (T.uv * wu - T.uu * wv) / T.D;                             // :148
+#endif
     if (tt < 0 || (s + tt) > 1) return;                                         // :149
     if (kStages) ++stg[4];
     const V3 e = sub(o, I);                                                     // distance, Vec3D.h:199-202
@@ -2716,6 +2741,8 @@ __global__ __launch_bounds__(kBlock) void k_assemble_pieces(const uint8_t *__res
 inline unsigned grid_for(int64_t n) { return static_cast<unsigned>((n + kBlock - 1) / kBlock); }
 
 }  // namespace
+
+bool tri_rcp_records() { return RT_TRI_RCP != 0; }   // the records' D slot holds rD (test_triangle)
 
 // The geometry's divisors as multiply-high magic numbers (fastdiv.h), for the kernels' index decoding.
 static FrameGeom with_divisors(FrameGeom g) {

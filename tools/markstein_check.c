@@ -3,7 +3,7 @@
  * (the first 64 structured, the rest hashed from SEED); scaling by powers of two is exact, so this covers
  * all quotients whose intermediates stay normal. Build: gcc -O3 -march=native -mfma -ffp-contract=off
  * -fopenmp tools/markstein_check.c -lm; run: ./a.out NDIV SEED. r05: 8192 divisors, 6.9e10 cases, 0 wrong
- * (the uncorrected q: 18.5% wrong). Groundwork for a cheaper s, t division. */
+ * (the uncorrected q: 18.5% wrong). tools/markstein_gpu.hip sweeps all 2^46 pairs on the GPU. */
 #include <math.h>
 #include <stdio.h>
 #include <stdint.h>
