@@ -528,6 +528,9 @@ __device__ __forceinline__ float cull_param(const Ray4 &R, float best, float pad
 #ifndef RT_ALWAYS_SORT
 #define RT_ALWAYS_SORT 0   // closest-hit: sort every node's keys (no nh count, no one-child branch)
 #endif
+#ifndef RT_ANY_ORDER
+#define RT_ANY_ORDER 0   // any-hit child order: 0 index order, 1 nearest entry first, 2 farthest first
+#endif
 #ifndef RT_TX_SLACK
 #define RT_TX_SLACK 1   // the 1e-5 relative slack of te <= tx (0: A/B measurement only)
 #endif
@@ -644,6 +647,20 @@ __device__ __forceinline__ int32_t node4_next(const Ray4 &R, const Node4Rows &nd
         return stack.pop_or(sp, base, kDoneRef);
     }
     // any-hit: any order finds the same verdict; visit the first wanted child, push the others
+#if RT_ANY_ORDER
+    {   // visit the nearest (1) or farthest (2) wanted child first, push the others
+        int kb = -1;
+        float tb = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (tc[k] != INFINITY && (kb < 0 || (RT_ANY_ORDER == 1 ? tc[k] < tb : tc[k] > tb))) { kb = k; tb = tc[k]; }
+#pragma unroll
+        for (int k = 3; k >= 0; --k)
+            if (tc[k] != INFINITY && k != kb) stack.push(sp, rc[k]);
+        if (kb >= 0) return rc[kb];
+        return stack.pop_or(sp, base, kDoneRef);
+    }
+#endif
     int32_t nxt = kDoneRef;
     bool have = false;
 #pragma unroll
