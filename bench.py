@@ -44,7 +44,7 @@ TILE = 16
 WORKLOADS = {
     "c4": dict(desc="C4: synthetic 8x8 UV-sphere grid OBJ (102,402 tris) 1920x1080, pf 1, depth 3, 2 lights",
                scene="syn:C4", width=1920, height=1080, pf=1, max_lvl=3, lights=((0.0, 0.0, 4.0), (1.5, 1.5, 4.0)),
-               cpu_every=96),
+               cpu_every=96, dropin=True, dropin_keys=("-", "-", "M:3", "A:1.5,1.5,4")),
     "c2": dict(desc="C2: dodgeColorTest.obj (16,311 tris) 800x600, pf 1, depth 1, 1 light",
                scene="ref:dodgeColorTest.obj", width=800, height=600, pf=1, max_lvl=1, lights=((0.0, 0.0, 4.0),),
                cpu_every=1),
@@ -122,6 +122,12 @@ def parse():
     ap.add_argument("--no-multi-frame", action="store_true", help="skip the rt_render_frames_device leg")
     ap.add_argument("--frames-per-call", type=int, default=4,
                     help="N=1 frame path: frames of the view per rt_render_frames_device call (one chain launch), 1-8")
+    ap.add_argument("--no-strong-shares", action="store_true",
+                    help="N=1: skip timing rank r's 1/N share of one frame for N = 2, 4, 8 (strong_shares)")
+    ap.add_argument("--no-e2e", action="store_true", help="N=1: skip the end-to-end frame (render -> host -> PPM file)")
+    ap.add_argument("--e2e-only", action="store_true", help="N=1: only the end-to-end frame leg (one JSON line)")
+    ap.add_argument("--e2e-frames", type=int, default=40, help="frames of the end-to-end leg per mode")
+    ap.add_argument("--ppm-threads", type=int, default=8, help="end-to-end leg: threads writing each PPM (rt_write_ppm_threads)")
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
                     help="extra launch-shape knob (Scene.tune), e.g. shadow_virtual=-1; repeatable")
     return ap.parse_args()
@@ -388,6 +394,13 @@ def main():
         scene.tune("frames_in_flight", inflight)
         main_run.fif = inflight
     calib = calibrate(inflight)
+    if args.e2e_only:   # the end-to-end leg alone (tools/gpu_run.sh e2e)
+        scene.tune("frames_in_flight", 1)
+        calibrate(1)
+        e2e = end_to_end(scene, cparams, WIDTH, HEIGHT, dev, frames=args.e2e_frames, threads=args.ppm_threads, workdir=tmp)
+        if rank == 0:
+            print(json.dumps({"metric": "end-to-end wall clock per frame", "workload": wl["desc"], "end_to_end": e2e}), flush=True)
+        return
     fpc = max(1, min(args.frames_per_call, 8)) if main_run.single else 1
     main_run.fpc = fpc
     # ---- timed region (the metric) ----
@@ -463,8 +476,17 @@ def main():
     scene.tune("cold_estimate", 2)   # (the library default)
     cold_ms = sorted(cold)[1] * 1e3 if cold else None
     cold_screen_ms = sorted(cold_screen)[1] * 1e3 if cold_screen else None
+    # ---- strong scaling measured on this GPU: rank r's 1/N share of one frame, every r, N = 2, 4, 8 ----
+    shares = None
+    if world == 1 and args.accel == "bvh" and not args.no_strong_shares and not args.rehearse:
+        shares = strong_shares(scene, cparams, WIDTH, HEIGHT, dev)
     main_run.run(0, max(args.warmup, 3))   # re-learn the measured order before the other legs
     calibrate(1)                            # (and re-decide the launch trials the cold legs forgot)
+    # ---- end to end: render -> bytes in host memory -> result.ppm (main.cpp:347-405) ----
+    e2e = None
+    if world == 1 and not args.no_e2e and not args.rehearse:
+        e2e = end_to_end(scene, cparams, WIDTH, HEIGHT, dev, frames=args.e2e_frames, threads=args.ppm_threads, workdir=tmp)
+        main_run.run(0, max(args.warmup, 3))
 
     # ---- the same work through the other path: N=1 the shard path (tiles + un-permute, what
     # N>1 runs, minus the collective); N>1 strong scaling (one frame split over the ranks) ----
@@ -722,9 +744,19 @@ def main():
             "cpu_baseline": None,
         }
         result.update(extra)
+        if shares is not None:
+            result["strong_shares"] = dict(shares, what="rank r's 1/N share of ONE frame (rt_render_tiles_device, tiles r, "
+                                           "r + N, ...), every rank, rendered on this GPU after its batch order and launch "
+                                           "trials settled: ms = median launch, one at a time (HIP events); max_ms = the "
+                                           "slowest rank (the frame time at N before the gather); pipelined_ms = four frames' "
+                                           "shares per call, calls back to back, per frame; assemble_ms = rank 0's device "
+                                           "un-permute of N shards; max_batch_us = the share's longest wave batch")
+        if e2e is not None:
+            result["config"]["end_to_end"] = e2e
         if world == 1 and batches:
-            result["strong_model"] = strong_model(elapsed / args.steps * 1e3, batches["max_us"] / 1e3,
-                                                  extra.get("shard_path", {}).get("ms_per_step"), WIDTH * HEIGHT * 3)
+            result["strong_model"] = strong_model((one_in_flight or {}).get("ms_per_step") or elapsed / args.steps * 1e3,
+                                                  batches["max_us"] / 1e3, extra.get("shard_path", {}).get("ms_per_step"),
+                                                  WIDTH * HEIGHT * 3, shares=shares, t1_pipe_ms=elapsed / args.steps * 1e3)
         if rehearsal is not None:
             result["rehearsal"] = rehearsal
         if args.ppm and timed_last is not None:
@@ -861,32 +893,205 @@ def orbit_leg(scene, run, W, H, PF, MAX_LVL, LIGHTS, flags, args, inflight, obj,
             "_last": (last, corners[warm + K - 1])}
 
 
-def strong_model(t1_ms, crit_ms, shard_ms, frame_bytes, link_gbs=(50.0, 150.0), rccl_lat_ms=0.02, sync_ms=0.02):
-    """Per-frame time of ONE frame split over N GPUs (strong scaling), from one-GPU
-    measurements: each rank renders 1/N of the interleaved tiles, which cannot take less than the
-    frame's longest wave batch (its critical path, measured); then one RCCL gather to rank 0 over
-    xGMI (rank 0 receives frame_bytes / N from each of the N - 1 peers on its own link, at an
-    assumed 50-150 GB/s per link, plus a collective latency), the device un-permute (measured at
-    N = 1: the shard path minus the frame path) and a barrier.
+def strong_shares(scene, cparams, W, H, dev, ns=(2, 4, 8), reps=15, warm=12, pipelined_k=4, ranks=None):
+    """Strong scaling measured on one GPU: for N = 2/4/8, rank r's 1/N share of ONE frame
+    (rt_render_tiles_device, first = r, stride = N: what rank r renders when one frame is split over N
+    GPUs, main.cpp:369-395 has no cross-pixel state) is rendered on its own until its batch order and
+    launch trials have settled, then timed launch by launch (HIP events on the launch stream, each
+    launch synchronised: one frame's latency) and back to back (`pipelined_k` frames' shares per call:
+    a stream of frames). The frame time at N is bound by the slowest rank: `max_ms` over the ranks.
+    The device un-permute of N shards into the frame (rt_assemble_tiles_device) is timed the same way.
+    Returns a dict keyed n2/n4/n8."""
+    import numpy as np
+    import torch
+
+    import raytracert_amd as R
+    from raytracert_amd import dist as rdist
+    st = torch.cuda.current_stream(dev)
+    layout = rdist.TileLayout(W, H, TILE, TILE)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+
+    def timed_launch(fn):
+        ev[0].record(st)
+        fn()
+        ev[1].record(st)
+        torch.cuda.synchronize(dev)
+        return ev[0].elapsed_time(ev[1])
+
+    out = {}
+    for N in ns:
+        per_rank = []
+        plan_k = rdist.ShardPlan(layout, N, frames=pipelined_k)
+        buf = torch.zeros(max(layout.shard_bytes(N), plan_k.shard_bytes), dtype=torch.uint8, device=dev)
+        for r in (range(N) if ranks is None else [x for x in ranks if x < N]):
+            def call(k=1):
+                scene.render_tiles_device(cparams, TILE, TILE, r, N, buf.data_ptr(), buf.numel(), st.cuda_stream, frames=k)
+            n = 0
+            while n < 64 and scene.trials()["choice"] < 0:   # (the share's own launch trials: as calibrate())
+                call()
+                torch.cuda.synchronize(dev)
+                n += 1
+            for _ in range(warm):
+                call()
+            torch.cuda.synchronize(dev)
+            lat = sorted(timed_launch(call) for _ in range(reps))
+            bd = scene.batch_durations()
+            tr = scene.trials()
+            # pipelined: pipelined_k frames' shares per call (one launch), calls back to back
+            m = 0
+            while m < 64 and scene.trials()["choice"] < 0:
+                call(pipelined_k)
+                torch.cuda.synchronize(dev)
+                m += 1
+            for _ in range(3):
+                call(pipelined_k)
+            torch.cuda.synchronize(dev)
+            ev[0].record(st)
+            for _ in range(reps):
+                call(pipelined_k)
+            ev[1].record(st)
+            torch.cuda.synchronize(dev)
+            pip = ev[0].elapsed_time(ev[1]) / reps / pipelined_k
+            per_rank.append({"rank": r, "tiles": layout.tiles_of(r, N), "ms": round(lat[len(lat) // 2], 4),
+                             "min_ms": round(lat[0], 4), "pipelined_ms": round(pip, 4),
+                             "max_batch_us": round(float(bd.max()), 1) if bd.size else None,
+                             "batches": int(bd.size), "calib": n, "choice": tr["choice"], "steal": tr["wave_steal"],
+                             "dist": tr["chain_split"]})
+        # the un-permute of N one-frame shards on rank 0 (the bytes do not change its time)
+        gathered = torch.zeros(N * layout.shard_bytes(N), dtype=torch.uint8, device=dev)
+        frame = torch.zeros(H * W * 3, dtype=torch.uint8, device=dev)
+
+        def assemble():
+            R.assemble_tiles_device(dev.index or 0, W, H, TILE, TILE, 1, N, gathered.data_ptr(), gathered.numel(),
+                                    frame.data_ptr(), frame.numel(), st.cuda_stream)
+        assemble()
+        asm = sorted(timed_launch(assemble) for _ in range(reps))[reps // 2]
+        worst = max(per_rank, key=lambda d: d["ms"])
+        out[f"n{N}"] = {"max_ms": worst["ms"], "max_rank": worst["rank"],
+                        "mean_ms": round(float(np.mean([d["ms"] for d in per_rank])), 4),
+                        "pipelined_max_ms": max(d["pipelined_ms"] for d in per_rank),
+                        "assemble_ms": round(asm, 4), "ranks": per_rank}
+    return out
+
+
+def end_to_end(scene, cparams, W, H, dev, frames=40, threads=8, workdir=None):
+    """A frame as the reference's 'r' key ends it (main.cpp:347-405): the render, the bytes in host
+    memory (Image::_image's quantised bytes; here one device-to-host copy of the uint8 frame into pinned
+    memory), then writeImage("result.ppm") (rt_write_ppm_threads, `threads` writers, the same file as
+    rt_write_ppm; rt_write_ppm with one thread timed beside it). Two modes over `frames` frames:
+    one at a time (render, copy, write in sequence, each synchronised) and pipelined (frame i's copy on
+    a copy stream and its PPM write on the host overlap frame i + 1's render). Host wall clock."""
+    import numpy as np
+    import torch
+
+    import raytracert_amd as R
+    st = torch.cuda.current_stream(dev)
+    cs = torch.cuda.Stream(dev)
+    n = H * W * 3
+    fbs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(2)]
+    hbs = [torch.empty(n, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    path = os.path.join(workdir or tempfile.mkdtemp(prefix="rt_e2e_"), "result.ppm")
+    ev_r = [torch.cuda.Event() for _ in range(2)]
+    ev_c = [torch.cuda.Event() for _ in range(2)]
+
+    def render(i):
+        scene.render_frame_device(cparams, TILE, TILE, fbs[i % 2].data_ptr(), n, st.cuda_stream)
+        ev_r[i % 2].record(st)
+
+    def copy(i):
+        cs.wait_event(ev_r[i % 2])
+        with torch.cuda.stream(cs):
+            hbs[i % 2].copy_(fbs[i % 2], non_blocking=True)
+        ev_c[i % 2].record(cs)
+
+    def write(i, nt=threads):
+        ev_c[i % 2].synchronize()
+        R.write_ppm_ptr(path, W, H, hbs[i % 2].data_ptr(), nt)
+
+    # one at a time: each stage waits for the one before it (a host that renders, reads and saves)
+    parts = {"render": [], "copy": [], "write": [], "write_1thread": []}
+    for i in range(frames + 3):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        render(i)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        copy(i)
+        cs.synchronize()
+        t2 = time.perf_counter()
+        write(i)
+        t3 = time.perf_counter()
+        R.write_ppm_ptr(path, W, H, hbs[i % 2].data_ptr(), 1)
+        t4 = time.perf_counter()
+        if i >= 3:
+            for k, v in zip(parts, (t1 - t0, t2 - t1, t3 - t2, t4 - t3)):
+                parts[k].append(v * 1e3)
+    one = {k: round(float(np.median(v)), 4) for k, v in parts.items()}
+    one["ms_per_frame"] = round(one["render"] + one["copy"] + one["write"], 4)
+    # pipelined: frame i's copy and write overlap frame i + 1's render
+    def pipelined(count):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(count):
+            if i >= 2:
+                st.wait_event(ev_c[i % 2])   # (frame i reuses frame i - 2's device buffer)
+            render(i)
+            copy(i)
+            if i >= 1:
+                write(i - 1)
+        write(count - 1)
+        torch.cuda.synchronize(dev)
+        return time.perf_counter() - t0
+    pipelined(4)
+    el = pipelined(frames)
+    with open(path, "rb") as f:   # the last frame's file is the last frame's bytes
+        body = f.read()
+    ok = body[:len(f"P6\n{W} {H}\n255\n")] == f"P6\n{W} {H}\n255\n".encode() and \
+        np.array_equal(np.frombuffer(body, np.uint8, offset=len(body) - n), fbs[(frames - 1) % 2].cpu().numpy())
+    return {"what": "render -> uint8 frame in host memory (pinned, one device-to-host copy) -> result.ppm "
+                    "(rt_write_ppm_threads), as main.cpp:347-405 ends a frame; host wall clock, medians",
+            "frames": frames, "ppm_threads": threads, "one_at_a_time": one,
+            "pipelined": {"ms_per_frame": round(el / frames * 1e3, 4),
+                          "what": "frame i's copy (copy stream) and PPM write (host) overlap frame i + 1's render"},
+            "last_file_equals_frame": bool(ok)}
+
+
+def strong_model(t1_ms, crit_ms, shard_ms, frame_bytes, link_gbs=(50.0, 150.0), rccl_lat_ms=0.02, sync_ms=0.02, shares=None,
+                 t1_pipe_ms=None):
+    """Per-frame time of ONE frame split over N GPUs (strong scaling). With `shares`
+    (strong_shares, r06: every rank's 1/N share of the frame rendered and timed on this GPU) the
+    render is the slowest rank's measured share and the un-permute its measured time; without, the
+    r04 model: max(t1 / N, the frame's longest wave batch) and the shard path minus the frame path.
+    The gather stays a model (one GPU here): rank 0 receives frame_bytes / N from each peer on its
+    own xGMI link at an assumed 50-150 GB/s, plus a collective latency, then a barrier.
     Two readings: `latency` is one frame on its own (render, then gather, un-permute and barrier in
-    sequence); `pipelined` is the frame rate of a stream of frames as bench.py's --mode strong runs
-    it (step i's gather runs on the collective's stream and its un-permute on rank 0's side stream
-    while step i + 1 renders, Runner.step), so the per-frame time is the slowest of the three
-    stages plus the per-step barrier."""
+    sequence); `pipelined` is the frame rate of a stream of frames (bench.py's --mode strong: step i's
+    gather and un-permute overlap step i + 1's render; measured shares: four frames' shares per render
+    call), the slowest stage plus the barrier. Speedups: latency against t1_ms (one frame at a time on
+    one GPU), pipelined against t1_pipe_ms (the one-GPU frame rate of the timed loop; default t1_ms)."""
+    t1p = t1_pipe_ms or t1_ms
     assemble_ms = max(0.0, (shard_ms or t1_ms) - t1_ms)
-    out = {"inputs": {"t1_ms": round(t1_ms, 4), "critical_path_ms": round(crit_ms, 4), "assemble_ms": round(assemble_ms, 4),
+    out = {"inputs": {"t1_ms": round(t1_ms, 4), "t1_pipelined_ms": round(t1p, 4), "critical_path_ms": round(crit_ms, 4), "assemble_ms": round(assemble_ms, 4),
                       "frame_bytes": frame_bytes, "link_gbs": list(link_gbs), "rccl_latency_ms": rccl_lat_ms,
-                      "sync_ms": sync_ms}}
+                      "sync_ms": sync_ms, "render": "measured shares (strong_shares)" if shares else "modelled"}}
     for n in (2, 4, 8):
-        render = max(t1_ms / n, crit_ms)
+        sh = (shares or {}).get(f"n{n}")
+        if sh:
+            render, render_p, asm = sh["max_ms"], sh["pipelined_max_ms"], sh["assemble_ms"]
+            bound = "measured: the slowest rank's share"
+        else:
+            render = render_p = max(t1_ms / n, crit_ms)
+            asm = assemble_ms
+            bound = "critical path" if crit_ms >= t1_ms / n else "work / N"
         res = {}
         for bw in link_gbs:
             gather = frame_bytes / n / (bw * 1e9) * 1e3 + rccl_lat_ms
-            t = render + gather + assemble_ms + sync_ms
-            tp = max(render, gather, assemble_ms) + sync_ms
+            t = render + gather + asm + sync_ms
+            tp = max(render_p, gather, asm) + sync_ms
             res[f"{int(bw)}GBs"] = {"latency_ms_per_frame": round(t, 4), "latency_speedup": round(t1_ms / t, 2),
-                                    "pipelined_ms_per_frame": round(tp, 4), "pipelined_speedup": round(t1_ms / tp, 2)}
-        out[f"n{n}"] = {"render_ms": round(render, 4), "bound": "critical path" if crit_ms >= t1_ms / n else "work / N", **res}
+                                    "pipelined_ms_per_frame": round(tp, 4), "pipelined_speedup": round(t1p / tp, 2)}
+        out[f"n{n}"] = {"render_ms": round(render, 4), "render_pipelined_ms": round(render_p, 4), "assemble_ms": round(asm, 4),
+                        "bound": bound, **res}
     return out
 
 
@@ -969,15 +1174,19 @@ def dropin_loop(obj, wl):
     subprocess.run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-I" + os.path.join(HERE, "include"),
                     os.path.join(HERE, "tests", "cxx", "dropin_main.cpp"), "-L" + lib, "-lrtamd", "-Wl,-rpath," + lib,
                     "-o", exe], check=True)
-    # pf stays the reference's default 3 and max_lvl its 10 (the drop-in's globals); 'T' x2: the
-    # first frame includes the upload of the workspace
-    out = subprocess.run([exe, "keys", obj, str(wl["width"]), str(wl["height"]), os.path.join(d, "f"), "T", "T", "R",
-                          "P:2000", "H", "H"], check=True, capture_output=True, text=True, timeout=600).stdout.splitlines()
+    # ref_default: pf stays the reference's default 3 and max_lvl its 10 (the drop-in's globals); other
+    # workloads set theirs with the host's keys first (C4: '-' twice for pf 1, max_lvl 3, the second
+    # light); 'T' x2: the first frame includes the upload of the workspace; 'V:200' checks 200 of the
+    # frame's cached colours against the per-call path (trace() of the loop's own ray), bit for bit
+    keys = list(wl.get("dropin_keys", ())) + ["T", "T", "V:200", "R", "P:2000", "H", "H"]
+    out = subprocess.run([exe, "keys", obj, str(wl["width"]), str(wl["height"]), os.path.join(d, "f")] + keys,
+                         check=True, capture_output=True, text=True, timeout=600).stdout.splitlines()
     fr = [l.split() for l in out if l.startswith("frame ")]
     single = next(l.split() for l in out if l.startswith("single "))
     floor = [float(l.split()[7]) for l in out if l.startswith("hostfloor ")]
     loop_ms = float(fr[1][10])
     n = wl["width"] * wl["height"] * wl["pf"] ** 2
+    ver = next((l.split() for l in out if l.startswith("verify ")), None)
     return {"what": "main.cpp:355-395 unchanged (performRayTracing per sub-sample) over the drop-in header, "
                     f"{wl['width']}x{wl['height']} pf {wl['pf']} = {n} calls",
             "loop_ms": loop_ms, "first_loop_ms": float(fr[0][10]), "render_image_ms": float(fr[2][7]),
@@ -989,7 +1198,9 @@ def dropin_loop(obj, wl):
                                "arguments: the unchanged loop's own cost (two divisions and ~60 flops per call)",
             "single_call_us": float(single[4]), "single_calls": int(single[1]),
             "per_call_loop_estimate_s": round(float(single[4]) * n / 1e6, 1),
-            "frames_equal": open(fr[1][1], "rb").read() == open(fr[2][1], "rb").read()}
+            "frames_equal": open(fr[1][1], "rb").read() == open(fr[2][1], "rb").read(),
+            "keys": keys,
+            "cached_vs_per_call": ({"records": int(ver[1]), "ray_diff": int(ver[4]), "rgb_diff": int(ver[6])} if ver else None)}
 
 
 def host_cpu():

@@ -605,11 +605,15 @@ struct TraceState {
         for (size_t i = 0; i < nl; ++i) x |= diff3(a[i].p, b[i].p);
         return x == 0;
     }
+    // the bits of one float, loaded as a 32-bit word (no copy through a stack array: an 8-byte load
+    // of two floats just stored one by one misses store forwarding, ~15 cycles a time on x86)
+    static uint32_t bits(const float *f) {
+        uint32_t u;
+        std::memcpy(&u, f, 4);
+        return u;
+    }
     static uint32_t diff3(const float *a, const float *b) {   // 0 when the three floats are the same bits
-        uint32_t u[3], v[3];
-        std::memcpy(u, a, 12);
-        std::memcpy(v, b, 12);
-        return (u[0] ^ v[0]) | (u[1] ^ v[1]) | (u[2] ^ v[2]);
+        return (bits(a) ^ bits(b)) | (bits(a + 1) ^ bits(b + 1)) | (bits(a + 2) ^ bits(b + 2));
     }
     static bool same_bits3(const float *a, const float *b) { return diff3(a, b) == 0; }
 };
@@ -637,18 +641,14 @@ struct FrameCache {
     float *rec = nullptr;     // 9 floats per sub-sample: origin, dest, rgb (pinned host memory)
     size_t rec_cap = 0;
     size_t host_ray_frames = 0;   // frames whose records hold host-made rays (the host rounds differently)
+    size_t device_frames = 0;     // frame traces made on the device (rt_trace_frame_samples)
     bool host_rays = false;       // this frame's records are host-made
     Vec3Df c[8];                  // this frame's corner rays (produceRay) and divisors
     float divX = 0, divY = 0;
     ~FrameCache() { rt_host_free(rec); }
     bool matches(const Vec3Df &o, const Vec3Df &d) const {   // the call's ray is record `next`'s, bit for bit
-        uint32_t a[6], b[6];
-        std::memcpy(a, o.p, 12);
-        std::memcpy(a + 3, d.p, 12);
-        std::memcpy(b, rec + 9 * next, 24);
-        uint32_t x = 0;
-        for (int i = 0; i < 6; ++i) x |= a[i] ^ b[i];
-        return x == 0;
+        const float *r = rec + 9 * next;
+        return (TraceState::diff3(o.p, r) | TraceState::diff3(d.p, r + 3)) == 0;
     }
     Vec3Df take() {
         const float *c = rec + 9 * next++ + 6;
@@ -666,23 +666,25 @@ inline FrameCache &frame_cache() {
 // -ffp-contract=fast on an FMA target): make every sub-sample's ray of the cached frame with loop_ray,
 // compiled into this translation unit with the host's own flags like its loop, and trace exactly those
 // in one call (records from `next` on are then the loop's own rays and their colours).
-inline void trace_host_rays(FrameCache &fc) {
-    const size_t n = fc.n;
-    std::vector<float> o(3 * n), d(3 * n), rgb(3 * n);
-    size_t k = 0;
-    for (unsigned y = 0; y < WindowSize_Y; ++y)
-        for (unsigned x = 0; x < WindowSize_X; ++x)
-            for (int sx = 0; sx < static_cast<int>(pixelfactorX); ++sx)
-                for (int sy = 0; sy < static_cast<int>(pixelfactorY); ++sy, ++k) {
-                    Vec3Df ro, rd;
-                    loop_ray(x, y, sx, sy, fc.divX, fc.divY, fc.c, ro, rd);
-                    std::memcpy(&o[3 * k], ro.p, 12);
-                    std::memcpy(&d[3 * k], rd.p, 12);
-                }
-    const rt_params p = params(max_lvl);
-    check(rt_trace_rays(scene(), &p, o.data(), d.data(), static_cast<int32_t>(n), rgb.data(), nullptr));
-    for (k = 0; k < n; ++k) {
-        float *r = fc.rec + 9 * k;
+// Records `from` .. n - 1 only: the records before `from` were answered already (resume_frame).
+inline void trace_host_rays(FrameCache &fc, size_t from = 0) {
+    const size_t n = fc.n, m = n > from ? n - from : 0;
+    const size_t spp = static_cast<size_t>(pixelfactorX) * pixelfactorY;
+    std::vector<float> o(3 * m), d(3 * m), rgb(3 * m);
+    for (size_t k = 0; k < m; ++k) {   // record from + k: pixel (from + k) / spp, sub-sample (subx, suby) in loop order
+        const size_t s = from + k, pix = s / spp, sub = s % spp;
+        Vec3Df ro, rd;
+        loop_ray(static_cast<unsigned>(pix % WindowSize_X), static_cast<unsigned>(pix / WindowSize_X),
+                 static_cast<int>(sub / pixelfactorY), static_cast<int>(sub % pixelfactorY), fc.divX, fc.divY, fc.c, ro, rd);
+        std::memcpy(&o[3 * k], ro.p, 12);
+        std::memcpy(&d[3 * k], rd.p, 12);
+    }
+    if (m > 0) {
+        const rt_params p = params(max_lvl);
+        check(rt_trace_rays(scene(), &p, o.data(), d.data(), static_cast<int32_t>(m), rgb.data(), nullptr));
+    }
+    for (size_t k = 0; k < m; ++k) {
+        float *r = fc.rec + 9 * (from + k);
         std::memcpy(r, &o[3 * k], 12);
         std::memcpy(r + 3, &d[3 * k], 12);
         std::memcpy(r + 6, &rgb[3 * k], 12);
@@ -705,13 +707,25 @@ inline bool start_frame(const Vec3Df &origin, const Vec3Df &dest) {
     loop_ray(0, 0, 0, 0, divX, divY, c, o0, d0);
     if (!same_bits(o0, origin) || !same_bits(dest, d0)) return false;
     FrameCache &fc = frame_cache();
-    fc.n = fc.next = 0;
     const size_t n = static_cast<size_t>(WindowSize_X) * WindowSize_Y * pixelfactorX * pixelfactorY;
+    // The previous frame needed the host's own rays (the host rounds its loop differently from the
+    // device) and nothing it depends on has changed since: this frame's rays are the host's too, so the
+    // device's frame trace would be thrown away: trace the host's rays directly.
+    bool same_view = fc.host_rays && fc.n == n && same_bits(Vec3Df(divX, divY, 0), Vec3Df(fc.divX, fc.divY, 0)) &&
+                     fc.state.matches_globals();
+    for (int i = 0; i < 8 && same_view; ++i) same_view = same_bits(c[i], fc.c[i]);
+    fc.n = fc.next = 0;
     ensure_records(fc.rec, fc.rec_cap, 9 * n);
+    if (same_view) {
+        fc.n = n;
+        trace_host_rays(fc);
+        return fc.matches(origin, dest);
+    }
     rt_params p = params(max_lvl);
     for (int i = 0; i < 8; ++i)
         for (int k = 0; k < 3; ++k) p.corners[i][k] = c[i][k];
     check(rt_trace_frame_samples(scene(), &p, RT_SAMPLES_RAY_RGB, fc.rec, fc.rec_cap, nullptr));
+    ++fc.device_frames;
     fc.state = TraceState::now();
     fc.n = n;
     fc.host_rays = false;
@@ -734,7 +748,7 @@ inline bool resume_frame(const Vec3Df &origin, const Vec3Df &dest) {
     loop_ray(static_cast<unsigned>(pix % WindowSize_X), static_cast<unsigned>(pix / WindowSize_X),
              static_cast<int>(sub / pixelfactorY), static_cast<int>(sub % pixelfactorY), fc.divX, fc.divY, fc.c, o, d);
     if (!same_bits(o, origin) || !same_bits(d, dest)) return false;
-    trace_host_rays(fc);
+    trace_host_rays(fc, fc.next);   // (the records before `next` were answered already)
     return fc.matches(origin, dest);
 }
 

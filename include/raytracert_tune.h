@@ -182,6 +182,10 @@ int rt_batch_durations(rt_scene *scene, uint32_t *ticks, int64_t capacity, int64
  * sq_dst, shadow, chain_local, chain_coef, depth, counters[0], counters[1], wq, cost[0], order[0],
  * cost[1], order[1], order_scratch. For tests of the sizing. */
 #define RT_WS_ARRAYS 22
+/* The render workspaces a scene holds now (every pipeline's), in bytes, and how many
+ * rt_render_frames_device calls fell back to rendering their frames one by one because the one-launch
+ * workspace could not be allocated (its frames' chain records past the LDS ones). */
+int rt_workspace_bytes(rt_scene *s, uint64_t *bytes, uint64_t *multi_frame_fallbacks);
 int rt_workspace_layout(int64_t cap, int32_t steps, int32_t lights, uint64_t *total_bytes,
                         uint64_t extents[2 * RT_WS_ARRAYS]);
 

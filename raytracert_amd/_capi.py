@@ -123,6 +123,7 @@ _SIGNATURES = {
                                 C.c_size_t, _VP, C.POINTER(C.c_int32), _VP], C.c_int),
     "rt_default_corners": ([C.c_int32, C.c_int32, _VP], C.c_int),
     "rt_write_ppm": ([C.c_char_p, C.c_int32, C.c_int32, _VP], C.c_int),
+    "rt_write_ppm_threads": ([C.c_char_p, C.c_int32, C.c_int32, _VP, C.c_int32], C.c_int),
     "rt_set_profiling": ([_VP, C.c_int32], C.c_int),
     "rt_kernel_stats": ([_VP, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.POINTER(C.c_double)], C.c_int),
     "rt_reset_stats": ([_VP], C.c_int),
@@ -132,6 +133,7 @@ _SIGNATURES = {
     "rt_scene_bvh_info": ([_VP, _VP], C.c_int),
     "rt_work_detail": ([_VP, C.c_int32, _VP], C.c_int),
     "rt_diag_read": ([_VP, C.c_int64, C.c_int64, _VP], C.c_int),
+    "rt_workspace_bytes": ([_VP, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)], C.c_int),
     "rt_workspace_layout": ([C.c_int64, C.c_int32, C.c_int32, C.POINTER(C.c_uint64), _VP], C.c_int),
     "rt_batch_durations": ([_VP, _VP, C.c_int64, C.POINTER(C.c_int64)], C.c_int),
     "rt_scene_trials": ([_VP, _VP, _VP], C.c_int),

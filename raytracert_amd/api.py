@@ -37,6 +37,12 @@ def write_ppm(path: str, rgb_u8: np.ndarray) -> None:
     check(lib().rt_write_ppm(path.encode(), w, h, _ptr(rgb)))
 
 
+def write_ppm_ptr(path: str, width: int, height: int, host_ptr: int, threads: int = 1) -> None:
+    """rt_write_ppm_threads from a host address (e.g. a pinned torch tensor's data_ptr()): the same
+    file as write_ppm, written by `threads` threads."""
+    check(lib().rt_write_ppm_threads(path.encode(), width, height, C.c_void_p(host_ptr), threads))
+
+
 @dataclass
 class RenderParams:
     """Everything the reference reads from globals during a render (raytracing.cpp:15-29,
@@ -339,6 +345,13 @@ class Scene:
              "inflight_streams": _capi.TUNE_INFLIGHT_STREAMS, "quad_walk": _capi.TUNE_QUAD_WALK,
              "motion_order": _capi.TUNE_MOTION_ORDER}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
+
+    def workspace_bytes(self) -> tuple[int, int]:
+        """rt_workspace_bytes: (bytes of the render workspaces held now, multi-frame calls that fell back to
+        rendering frame by frame)."""
+        b, f = C.c_uint64(), C.c_uint64()
+        check(lib().rt_workspace_bytes(self._h, C.byref(b), C.byref(f)))
+        return b.value, f.value
 
     def trials(self) -> dict:
         """rt_scene_trials: the per-view launch trials (steal x distribution x shadow helpers) of

@@ -132,6 +132,8 @@ struct DevWork {
     int32_t *order_scratch;         // counting-sort scratch (kOrderBuckets histogram, then offsets)
     int64_t cap;                    // samples per batch
     int32_t steps;                  // chain steps allocated (max_lvl + 1)
+    int64_t rec_cap;                // chain_local's samples per step: cap x the frames of a multi-frame launch whose
+                                    // records reach past the LDS ones (frame f's at sample + f x cap), else cap
 };
 
 constexpr int kMaxStepsCounters = 4096;   // counters[step] for main queues; [kMaxStepsCounters + step] shadow

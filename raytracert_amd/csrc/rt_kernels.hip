@@ -1678,11 +1678,11 @@ __device__ __forceinline__ float4 *lds_records() {
 }
 __device__ __forceinline__ void put_record(const DevWork &w, int step, int sample, float4 v) {
     if (RT_LDS_RECORDS > 0 && step < RT_LDS_RECORDS) lds_records()[step * kBvhBlock + static_cast<int>(threadIdx.x)] = v;
-    else store_chain(&w.chain_local[static_cast<int64_t>(step) * w.cap + sample], v);
+    else store_chain(&w.chain_local[static_cast<int64_t>(step) * w.rec_cap + sample], v);
 }
 __device__ __forceinline__ float4 get_record(const DevWork &w, int step, int sample) {
     if (RT_LDS_RECORDS > 0 && step < RT_LDS_RECORDS) return lds_records()[step * kBvhBlock + static_cast<int>(threadIdx.x)];
-    return w.chain_local[static_cast<int64_t>(step) * w.cap + sample];
+    return w.chain_local[static_cast<int64_t>(step) * w.rec_cap + sample];
 }
 
 // reflection (raytracing.cpp:277-285) + addOffset (:266-271): the traced ray of level `lvl`.
@@ -1734,7 +1734,7 @@ __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadePa
     sec.org = mk(0, 0, 0);
     sec.dst = mk(0, 0, 0);
     sec.lvl = -1;
-    const int64_t ci = static_cast<int64_t>(step) * w.cap + sample;
+    const int64_t ci = static_cast<int64_t>(step) * w.rec_cap + sample, cc = static_cast<int64_t>(step) * w.cap + sample;
     const float4 nw = sc.normals[idx];
     V3 normal = ld3(nw);                                             // :394 (copy, mutated below)
     // normal.normalize() (:199, :213): from the face's tabled states when it has them (k_normal_table)
@@ -1843,7 +1843,7 @@ __device__ __forceinline__ Secondary shade_hit(const DevScene &sc, const ShadePa
         return sec;
     }
     store_chain(&w.chain_local[ci], make_float4(color.x, color.y, color.z, as_float(static_cast<int>(sec.state))));
-    if (sec.state == kChildTrace) store_chain(&w.chain_coef[ci], make_float4(sec.coef.x, sec.coef.y, sec.coef.z, 0.0f));
+    if (sec.state == kChildTrace) store_chain(&w.chain_coef[cc], make_float4(sec.coef.x, sec.coef.y, sec.coef.z, 0.0f));
     else w.depth[sample] = static_cast<uint8_t>(step + 1);
     return sec;
 }
@@ -1865,7 +1865,7 @@ __device__ __forceinline__ V3 fold_inlane(const DevScene &sc, const DevWork &w, 
 
 // trace() miss (:389-391): black, and the chain ends at this step.
 __device__ __forceinline__ void shade_miss(const DevWork &w, int step, int sample) {
-    store_chain(&w.chain_local[static_cast<int64_t>(step) * w.cap + sample], make_float4(0, 0, 0, as_float(kChildNone)));
+    store_chain(&w.chain_local[static_cast<int64_t>(step) * w.rec_cap + sample], make_float4(0, 0, 0, as_float(kChildNone)));
     w.depth[sample] = static_cast<uint8_t>(step + 1);
 }
 
@@ -1914,11 +1914,10 @@ __device__ __forceinline__ V3 fold_chain(const DevWork &w, int64_t s) {
     V3 c = mk(0, 0, 0);
     const int d = w.depth[s];
     for (int k = d - 1; k >= 0; --k) {
-        const int64_t ci = static_cast<int64_t>(k) * w.cap + s;
-        const float4 L = w.chain_local[ci];
+        const float4 L = w.chain_local[static_cast<int64_t>(k) * w.rec_cap + s];
         const uint32_t st = static_cast<uint32_t>(as_int(L.w));
         if (st == kChildTrace) {
-            const float4 K = w.chain_coef[ci];
+            const float4 K = w.chain_coef[static_cast<int64_t>(k) * w.cap + s];
             c = add(mk(L.x, L.y, L.z), mul(mk(K.x, K.y, K.z), c));
         } else if (st == kChildZero) {
             c = add(mk(L.x, L.y, L.z), mk(0.0f, 0.0f, 0.0f));
@@ -2188,8 +2187,9 @@ __device__ __forceinline__ void quad_batch(const DevScene &sc, const ShadeParams
 // k_chain's explicit arguments as laid out in the kernel-argument segment (in order, each at its
 // natural alignment, as the members of a struct), for RT_OPAQUE_ARGS. The layout is a property of
 // the kernel's signature, so it is checked once per kernel instantiation rather than per launch:
-// probe_chain_kernargs launches k_chain in probe mode (ordered -1), which compares every argument
-// with the ChainKernargs member at its place (chain_kernarg_mismatch) and reports a bit per argument.
+// probe_chain_kernargs launches k_chain_kernarg_probe, a kernel with k_chain's exact parameter list,
+// which compares every argument with the ChainKernargs member at its place (chain_kernarg_mismatch)
+// and reports a bit per argument.
 #ifndef RT_KARGS_PERTURB
 #define RT_KARGS_PERTURB 0   // test build only (librtamd_kargperturb.so): a layout the probe must reject
 #endif
@@ -2208,6 +2208,9 @@ struct ChainKernargs {
     int split, split8;
     FrameSet fs;
 };
+// the kernel-argument segment is at most 4 KB (the scene, the shading parameters with 16 lights, the
+// workspace, the frame geometry and the multi-frame set are 2,032 B now): growth past it fails here
+static_assert(sizeof(ChainKernargs) <= 4096, "k_chain's arguments exceed the 4 KB kernel-argument segment");
 
 // Bit k set: argument k of k_chain is not where ChainKernargs places it. The probe launch fills each
 // by-value structure with a word pattern (word i of argument k = kKargTag[k] + i, padding included,
@@ -3034,6 +3037,10 @@ __device__ __forceinline__ int order_cell(const FrameGeom &g, int spb, int nq, i
     int x, y;
     uint32_t slot;
     decode_pixel(g, pix, x, y, slot);
+    // a batch whose middle sample lies in a tile's padding (past the frame's edge) takes the nearest
+    // cell inside the frame, so the index stays below cells_x x cells_y
+    x = min(max(x, 0), g.width - 1);
+    y = min(max(y, 0), g.height - 1);
     return (y >> 3) * cells_x + (x >> 3);
 }
 __global__ __launch_bounds__(kBlock) void k_order_cells(const uint32_t *__restrict__ cost, int n, const FrameGeom g, int spb, int nq,

@@ -297,9 +297,43 @@ int main(int argc, char **argv) {
             render_one_call();
         } else if (k[0] == 'T') {
             render_r(true);
-            std::printf("cache host_ray_frames %zu\n", rtamd_dropin::frame_cache().host_ray_frames);
+            std::printf("cache host_ray_frames %zu device_frames %zu\n", rtamd_dropin::frame_cache().host_ray_frames,
+                        rtamd_dropin::frame_cache().device_frames);
         } else if (k[0] == 'H') {
             render_host_floor();
+        } else if (k[0] == 'M' && k[1] == ':') {   // max_lvl (raytracing.cpp:29) set by the host, e.g. a BASELINE config
+            max_lvl = std::atoi(k + 2);
+        } else if (k[0] == 'A' && k[1] == ':') {   // a light at a given position (as 'L' appends the camera's)
+            float x = 0, y = 0, z = 0;
+            std::sscanf(k + 2, "%f,%f,%f", &x, &y, &z);
+            MyLightPositions.push_back(Vec3Df(x, y, z));
+        } else if (k[0] == 'V' && k[1] == ':') {   // after a frame: N of its cached records against the per-call path
+            // (the loop's own ray for the record, made by this translation unit as the loop makes it, and
+            // trace(origin, dest, 0): one rt_trace_rays of that ray)
+            const int n = std::atoi(k + 2);
+            const rtamd_dropin::FrameCache &fc = rtamd_dropin::frame_cache();
+            Vec3Df c[8];
+            produceRay(0, 0, c[0], c[1]);
+            produceRay(0, WindowSize_Y - 1, c[2], c[3]);
+            produceRay(WindowSize_X - 1, 0, c[4], c[5]);
+            produceRay(WindowSize_X - 1, WindowSize_Y - 1, c[6], c[7]);
+            const float divX = (WindowSize_X * pixelfactorX - 1), divY = (WindowSize_Y * pixelfactorY - 1);
+            const size_t spp = size_t(pixelfactorX) * pixelfactorY;
+            int ray_diff = 0, rgb_diff = 0;
+            for (int j = 0; j < n && fc.n > 0; ++j) {
+                const size_t s = (fc.n - 1) * size_t(j) / size_t(n > 1 ? n - 1 : 1), pix = s / spp, sub = s % spp;
+                const unsigned x = unsigned(pix % WindowSize_X), y = unsigned(pix / WindowSize_X);
+                const int subx = int(sub / pixelfactorY), suby = int(sub % pixelfactorY);
+                float xscale = 1.0f - (float(x) * pixelfactorX + subx) / divX;   // main.cpp:380-386, as render_r
+                float yscale = 1.0f - (float(y) * pixelfactorY + suby) / divY;
+                Vec3Df origin = yscale * (xscale * c[0] + (1 - xscale) * c[4]) + (1 - yscale) * (xscale * c[2] + (1 - xscale) * c[6]);
+                Vec3Df dest = yscale * (xscale * c[1] + (1 - xscale) * c[5]) + (1 - yscale) * (xscale * c[3] + (1 - xscale) * c[7]);
+                const float *r = fc.rec + 9 * s;
+                ray_diff += std::memcmp(r, origin.p, 12) != 0 || std::memcmp(r + 3, dest.p, 12) != 0;
+                const Vec3Df t = trace(origin, dest, 0);
+                rgb_diff += std::memcmp(r + 6, t.p, 12) != 0;
+            }
+            std::printf("verify %d records ray_diff %d rgb_diff %d host_rays %d\n", n, ray_diff, rgb_diff, fc.host_rays ? 1 : 0);
         } else if (k[0] == 'P' && k[1] == ':') {   // single calls off the frame cache (rays of no frame)
             const int n = std::atoi(k + 2);
             Vec3Df o00, d00, o11, d11, acc;

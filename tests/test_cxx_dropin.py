@@ -161,10 +161,13 @@ def test_dropin_literal_loop_uses_one_gpu_call_per_frame(dropin_bin, workdir, tm
     trace, so the loop takes well under a second, and its frame equals renderImage()'s."""
     path = scene_path("ref:dodgeColorTest.obj", workdir)
     prefix = str(tmp_path / "g")
-    lines = _lines([dropin_bin, "keys", path, "500", "500", prefix, "T", "R", "P:300"])
+    lines = _lines([dropin_bin, "keys", path, "500", "500", prefix, "T", "V:200", "R", "P:300"])
     fr = [l.split() for l in lines if l.startswith("frame ")]
     assert float(fr[0][10]) < 5000.0   # ms: the whole literal loop
     assert np.array_equal(read_ppm(fr[0][1]), read_ppm(fr[1][1]))
+    # 200 records of the frame against the per-call path (the loop's own ray, trace() of it): bit for bit
+    v = next(l.split() for l in lines if l.startswith("verify "))
+    assert v[1] == "200" and v[4] == "0" and v[6] == "0" and v[8] == "0", v
     single = next(l.split() for l in lines if l.startswith("single "))
     assert float(single[4]) > 0
 
@@ -224,12 +227,18 @@ def test_dropin_loop_with_fma_contraction_still_uses_frame_trace(workdir, tmp_pa
     exe = _build(str(tmp_path / "dropin_fma"), ["-mfma", "-ffp-contract=fast", "-I" + os.path.join(ROOT, "include")])
     path = scene_path("ref:dodgeColorTest.obj", workdir)
     # (bounded: the per-call path would take ~150 s per frame)
-    r = subprocess.run([exe, "keys", path, "500", "500", str(tmp_path / "c"), "T", "T", "R"], check=True, capture_output=True,
-                       text=True, timeout=120)
+    r = subprocess.run([exe, "keys", path, "500", "500", str(tmp_path / "c"), "T", "T", "V:200", "R"], check=True,
+                       capture_output=True, text=True, timeout=120)
     lines = r.stdout.splitlines()
     fr = [l.split() for l in lines if l.startswith("frame ")]
-    cache = [int(l.split()[2]) for l in lines if l.startswith("cache host_ray_frames")]
+    cache = [(int(l.split()[2]), int(l.split()[4])) for l in lines if l.startswith("cache host_ray_frames")]
     assert float(fr[1][10]) < 5000.0, fr[1]
-    assert cache[-1] >= 1, "the FMA build's rays matched the device's: this test no longer covers the fallback"
+    assert cache[-1][0] >= 1, "the FMA build's rays matched the device's: this test no longer covers the fallback"
+    # the second frame of the same view goes straight to the host's rays (one device frame
+    # trace in the session, the first frame's, whose rays turned out not to be the loop's)
+    assert cache[0][1] == 1 and cache[1][1] == 1, cache
     loop, one = read_ppm(fr[1][1]), read_ppm(fr[2][1])
     assert (loop == one).mean() >= 0.999
+    # the cached colours are trace() of the host's own rays, bit for bit (the per-call path, 200 records)
+    v = next(l.split() for l in lines if l.startswith("verify "))
+    assert v[1] == "200" and v[4] == "0" and v[6] == "0" and v[8] == "1", v

@@ -66,6 +66,30 @@ def test_frames_in_one_launch_equal_single_frames(name, knobs, workdir, gpu_avai
         assert np.array_equal(img[y0:y0 + 16, x0:x0 + 16], ou8)
 
 
+def test_multiframe_workspace_grows_by_the_deep_records_only(workdir, gpu_available):
+    """eight views at the reference's defaults (max_lvl 10: chain records past the three
+    LDS steps) in one launch keep each frame's deep records at sample + frame x samples in chain_local;
+    only that array grows with the frames (7 more frames x 2.25M samples x 11 steps x 16 B), not the
+    whole ~1 GB per-frame workspace (~8.5 GB before), and the call renders in one launch (no fallback)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    views = _views(REF, 8)
+    cap, steps = REF["w"] * REF["h"] * REF["pf"] ** 2, REF["max_lvl"] + 1
+    with R.Scene.load(scene_path(REF["spec"], workdir), device=0) as sc:
+        one, _ = _single(sc, torch, dev, views[7])
+        torch.cuda.synchronize(dev)
+        b1, f1 = sc.workspace_bytes()
+        bufs = [torch.zeros(REF["h"] * REF["w"] * 3, dtype=torch.uint8, device=dev) for _ in range(8)]
+        sc.render_frames_device(views, 16, 16, [b.data_ptr() for b in bufs], bufs[0].numel(),
+                                torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        b8, f8 = sc.workspace_bytes()
+        assert f1 == f8 == 0
+        assert b1 < b8 <= b1 + 7 * cap * steps * 16 + 4096, (b1, b8)
+        assert b8 < 4 * b1
+        assert torch.equal(bufs[7], one)
+
+
 def test_frames_in_one_launch_two_in_flight(workdir, gpu_available):
     """Two-frame calls on two streams with RT_TUNE_FRAMES_IN_FLIGHT 2 (each call on its own pipeline)."""
     import torch

@@ -55,6 +55,44 @@ def test_assemble_composes_interleaved_shards(nranks, frames, size, tile, workdi
     assert [int(x) for x in total] == [frames * int(x) for x in c1]
 
 
+@pytest.mark.parametrize("knobs", [{}, {"split_eighth": 4096}, {"quad_walk": 1, "steal_quarter": 4096}])
+def test_strong_shares_settled_reassemble_to_the_frame(knobs, workdir, gpu_available):
+    """bench.strong_shares' measurement: at N = 8 each rank's share of one C4 frame is
+    rendered until its batch order and launch trials have settled (ordered launches: the split tiers,
+    the trials' kernel and distribution), under the default and the wider split policies; the last
+    render of every share, laid out as one gather lays them out and un-permuted, is the one-GPU frame
+    byte for byte, and the shares' ray counts add up to the frame's."""
+    import torch
+    w, h, N = 1920, 1080, 8
+    p = R.RenderParams(width=w, height=h, pf=1, max_lvl=3, lights=LIGHTS)
+    T = (w // 16) * ((h + 15) // 16)
+    shard = ((T + N - 1) // N) * 16 * 16 * 3
+    stream = torch.cuda.current_stream().cuda_stream
+    with R.Scene.load(scene_path("syn:C4", workdir), device=0) as sc:
+        for k, v in knobs.items():
+            sc.tune(k, v)
+        full, c1 = _frame(sc, p)
+        gathered = torch.full((N * shard,), 7, dtype=torch.uint8, device="cuda:0")
+        total = np.zeros(3, np.uint64)
+        for r in range(N):
+            part = gathered[r * shard:(r + 1) * shard]
+            n = 0
+            while n < 64 and sc.trials()["choice"] < 0:
+                sc.render_tiles_device(p, 16, 16, r, N, part.data_ptr(), part.numel(), stream)
+                torch.cuda.synchronize()
+                n += 1
+            for _ in range(4):
+                sc.render_tiles_device(p, 16, 16, r, N, part.data_ptr(), part.numel(), stream)
+            _, c = sc.render_tiles_device(p, 16, 16, r, N, part.data_ptr(), part.numel(), stream, want_counts=True)
+            total += c
+            assert sc.trials()["choice"] >= 0, (r, n)
+        out = torch.zeros(h * w * 3, dtype=torch.uint8, device="cuda:0")
+        R.assemble_tiles_device(0, w, h, 16, 16, 1, N, gathered.data_ptr(), gathered.numel(), out.data_ptr(), out.numel(), stream)
+        got = out.view(h, w, 3).cpu().numpy()
+    assert np.array_equal(got, full)
+    assert [int(x) for x in total] == [int(x) for x in c1]
+
+
 def test_render_frames_sharded_world1(workdir, gpu_available):
     import torch
     comm = R.Comm(0, 0, 1, R.Comm.unique_id())
