@@ -121,7 +121,11 @@ def parse():
                          "(scenes.orbit_corners; 0 = skip): config.orbit")
     ap.add_argument("--no-multi-frame", action="store_true", help="skip the rt_render_frames_device leg")
     ap.add_argument("--frames-per-call", type=int, default=4,
-                    help="N=1 frame path: frames of the view per rt_render_frames_device call (one chain launch), 1-8")
+                    help="N=1 frame path: frames per rt_render_frames_device call (one chain launch), 1-8")
+    ap.add_argument("--camera-path", type=float, default=0.25,
+                    help="N=1 with --frames-per-call > 1: the frames of a call are consecutive views of a camera path "
+                         "around the default view (turned -4..4 x this many degrees about y, a triangle wave of period "
+                         "16), so no two frames of a call are the same view (ADVICE r05); 0 = the same view K times")
     ap.add_argument("--no-strong-shares", action="store_true",
                     help="N=1: skip timing rank r's 1/N share of one frame for N = 2, 4, 8 (strong_shares)")
     ap.add_argument("--no-e2e", action="store_true", help="N=1: skip the end-to-end frame (render -> host -> PPM file)")
@@ -242,6 +246,11 @@ def main():
             self.total = 0   # frames of the current run's timed steps (frame path: steps are calls of fpc frames)
             self.nfin = 0
             self.pending = []
+            self.path = None       # camera path views (c params) of the multi-frame headline, and their ray counts
+            self.path_rays = None
+            self.pidx = 0          # next path position
+            self.rays_acc = 0      # rays of the path views rendered since the last reset
+            self.last_pos = 0      # path position of the last rendered frame
             # rank 0 un-permutes on a side stream, so the next step's render is not queued behind it
             self.side = torch.cuda.Stream(dev) if (rank == 0 and not frame_path) else None
 
@@ -287,7 +296,15 @@ def main():
             base = (i % 2) * self.fpc
             st = self.fstreams[i % self.fif]
             bufs = self.fbufs[base:base + k]
-            scene.render_frames_device([cparams] * k, TILE, TILE, [b.data_ptr() for b in bufs], bufs[0].numel(), st.cuda_stream)
+            if self.path is None:
+                views = [cparams] * k
+            else:   # k consecutive views of the camera path
+                pos = [(self.pidx + j) % len(self.path) for j in range(k)]
+                views = [self.path[m] for m in pos]
+                self.rays_acc += sum(self.path_rays[m] for m in pos)
+                self.pidx += k
+                self.last_pos = pos[-1]
+            scene.render_frames_device(views, TILE, TILE, [b.data_ptr() for b in bufs], bufs[0].numel(), st.cuda_stream)
             return bufs[-1]
 
         def step(self, i, k=1):
@@ -327,6 +344,7 @@ def main():
             for i in range(warmup if self.single else max(1, warmup // self.kstep) if warmup else 0):
                 self.step(i, self.fpc)
             self.drain()
+            self.rays_acc = 0
             torch.cuda.synchronize(dev)
             if world > 1:
                 dist.barrier()
@@ -403,18 +421,46 @@ def main():
         return
     fpc = max(1, min(args.frames_per_call, 8)) if main_run.single else 1
     main_run.fpc = fpc
+    path_what = None
+    if fpc > 1 and args.camera_path > 0:
+        # the headline's camera path: view m of 16 = the default view turned by tri(m) x step degrees about
+        # the world y axis (the trackball's effect on produceRay, scenes.orbit_corners), tri = 0,1,..,4,3,..,-4,..,-1
+        tri = [m if m <= 4 else 8 - m if m <= 12 else m - 16 for m in range(16)]
+        main_run.path = [R.RenderParams(width=WIDTH, height=HEIGHT, pf=PF, max_lvl=MAX_LVL, lights=LIGHTS, flags=flags,
+                                        corners=scenes.orbit_corners(WIDTH, HEIGHT, t, args.camera_path)).to_c() for t in tri]
+        per_angle = {}
+        fbc = main_run.fbufs[0]
+        for t in sorted(set(tri)):
+            c = scene.render_frame_device(main_run.path[tri.index(t)], TILE, TILE, fbc.data_ptr(), fbc.numel(),
+                                          stream.cuda_stream, want_counts=True)
+            per_angle[t] = int(sum(int(x) for x in c))
+        main_run.path_rays = [per_angle[t] for t in tri]
+        path_what = {"views": 16, "distinct": len(per_angle), "step_deg": args.camera_path,
+                     "turn_deg": [round(t * args.camera_path, 4) for t in tri],
+                     "rays_per_view": {str(round(t * args.camera_path, 4)): r for t, r in per_angle.items()},
+                     "what": "the timed calls render consecutive views of this camera path around the default view "
+                             "(four distinct views per call); rays are counted per view"}
     # ---- timed region (the metric) ----
     elapsed, frames = main_run.run(args.steps, args.warmup * inflight)
     main_run.fpc = 1
     # the last timed frame, kept before any later leg reuses its buffer: the in-run parity check
-    # (cpu_baseline) reads this copy
+    # (cpu_baseline) reads this copy, at that frame's view (a camera-path view in the headline mode)
     timed_last = frames.clone() if frames is not None else None
+    timed_corners = timed_corners_deg = None
+    timed_rays = main_run.rays_acc if main_run.path is not None else None
+    if main_run.path is not None:
+        tri_last = [m if m <= 4 else 8 - m if m <= 12 else m - 16 for m in range(16)][main_run.last_pos]
+        timed_corners = scenes.orbit_corners(WIDTH, HEIGHT, tri_last, args.camera_path)
+        timed_corners_deg = round(tri_last * args.camera_path, 4)
+    headline_path = main_run.path
+    main_run.path = None   # (the other legs render the default view; the roofline's profiled calls the path again)
     torch.cuda.synchronize(dev)
-    timed_last_what = (f"the last frame of the last timed call ({fpc} frames per call, {inflight} call(s) in flight)"
+    timed_last_what = (f"the last frame of the last timed call ({fpc} frames per call, {inflight} call(s) in flight"
+                       + (f", camera-path view turned {timed_corners_deg} degrees)" if timed_corners is not None else ")")
                        if main_run.single else f"timed step {args.steps - 1} of {args.steps} (the assembled frame on rank 0)")
     one_in_flight = in_flight = None
     value_mode = (f"{fpc}_frames_per_call" if fpc > 1 else "") + (f"{'_' if fpc > 1 else ''}{inflight}_in_flight" if inflight > 1 else "")
-    value_mode = value_mode or "one_in_flight"
+    value_mode = (value_mode or "one_in_flight") + ("_camera_path" if timed_rays else "")
     if main_run.single and (inflight > 1 or fpc > 1):   # the same frames one at a time (each frame's own latency)
         scene.tune("frames_in_flight", 1)
         main_run.fif = 1
@@ -511,8 +557,10 @@ def main():
         def one(i):
             if k > 1 and runner.single:
                 runner.fpc = k
+                runner.path = headline_path
                 runner.render_call(i, k)
                 runner.fpc = 1
+                runner.path = None
             else:
                 runner.render_once(i)
         scene.tune("pipes", 1)
@@ -585,7 +633,7 @@ def main():
 
     result = None
     if rank == 0:
-        total_rays = rays_per_step * args.steps
+        total_rays = timed_rays if timed_rays else rays_per_step * args.steps
         value = total_rays / elapsed / 1e6
         queries = ch_tests / max(nt, 1)
         per_rank_steps = args.profile_steps * (fpc if main_run.single else kstep)   # frames (of steps) in the profiled launches
@@ -690,9 +738,11 @@ def main():
                 "one_in_flight": one_in_flight,
                 "in_flight": in_flight,
                 "frames_per_call": fpc,
-                "frames_per_call_what": "frames of the view rendered by one rt_render_frames_device call: one chain launch "
-                                        "whose wave tasks cycle over the frames (the frames overlap on one stream and one "
-                                        "hardware queue); ms_per_step = wall clock / frames",
+                "frames_per_call_what": "frames rendered by one rt_render_frames_device call: one chain launch whose wave "
+                                        "tasks cycle over the frames (the frames overlap on one stream and one hardware "
+                                        "queue); with camera_path, consecutive distinct views of the path; ms_per_step = "
+                                        "wall clock / frames",
+                "camera_path": path_what,
                 "orbit": orbit,
                 "multi_frame": multi_frame,
                 "first_frame_ms": round(cold_ms, 3) if cold_ms is not None else None,
@@ -768,7 +818,7 @@ def main():
 
     # ---- CPU baseline + in-run parity on a bounded tile sample (rank 0, N=1 only) ----
     if rank == 0 and world == 1 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(obj, params, timed_last[0].cpu().numpy(), layout, args, wl)
+        result["cpu_baseline"] = cpu_baseline(obj, params, timed_last[0].cpu().numpy(), layout, args, wl, corners=timed_corners)
         result["cpu_baseline"]["parity_vs_gpu"]["frame"] = timed_last_what
         if orbit_last is not None:   # the last timed orbit view, on tiles across its sphere region
             result["config"]["orbit"]["parity_vs_cpu"] = orbit_parity(obj, params, orbit_last, wl)
@@ -789,8 +839,9 @@ def multiframe_leg(scene, run, cparams, W, H, args, rays_per_frame, dev):
     import torch
     K_MAX = 8
     bufs = [torch.zeros(H * W * 3, dtype=torch.uint8, device=dev) for _ in range(2 * K_MAX)]
-    out = {"what": "K frames of the view per rt_render_frames_device call (one chain launch whose wave tasks cycle "
-                   "over the frames), calls back to back; every frame fully rendered"}
+    out = {"what": "K frames of the SAME (default) view per rt_render_frames_device call (one chain launch whose wave "
+                   "tasks cycle over the frames), calls back to back; every frame fully rendered (identical copies: the "
+                   "headline's calls render distinct camera-path views instead)"}
     for K, fif in ((2, 1), (4, 1), (8, 1), (2, 2), (4, 2)):
         scene.tune("frames_in_flight", fif)
         calls = max(args.steps // K, 2)
@@ -926,7 +977,9 @@ def strong_shares(scene, cparams, W, H, dev, ns=(2, 4, 8), reps=15, warm=12, pip
         for r in (range(N) if ranks is None else [x for x in ranks if x < N]):
             def call(k=1):
                 scene.render_tiles_device(cparams, TILE, TILE, r, N, buf.data_ptr(), buf.numel(), st.cuda_stream, frames=k)
-            n = 0
+            call()   # (a new batch geometry: its first launch resets the trials trials() reports)
+            torch.cuda.synchronize(dev)
+            n = 1
             while n < 64 and scene.trials()["choice"] < 0:   # (the share's own launch trials: as calibrate())
                 call()
                 torch.cuda.synchronize(dev)
@@ -938,7 +991,9 @@ def strong_shares(scene, cparams, W, H, dev, ns=(2, 4, 8), reps=15, warm=12, pip
             bd = scene.batch_durations()
             tr = scene.trials()
             # pipelined: pipelined_k frames' shares per call (one launch), calls back to back
-            m = 0
+            call(pipelined_k)
+            torch.cuda.synchronize(dev)
+            m = 1
             while m < 64 and scene.trials()["choice"] < 0:
                 call(pipelined_k)
                 torch.cuda.synchronize(dev)
@@ -1243,7 +1298,7 @@ def orbit_parity(obj, params, last, wl):
             "frame": "the last timed orbit view"}
 
 
-def cpu_baseline(obj, params, gpu_frame, layout, args, wl):
+def cpu_baseline(obj, params, gpu_frame, layout, args, wl, corners=None):
     """Time the CPU restatement (oracle/, 'port') on every k-th 16x16 tile of the same frame (C2:
     the whole frame) with --cpu-threads threads, and on every --cpu-single-every-th of those tiles
     with one thread; check the GPU's bytes on the sampled tiles against it."""
@@ -1252,7 +1307,7 @@ def cpu_baseline(obj, params, gpu_frame, layout, args, wl):
     import oracle as O
     sc = O.OracleScene(obj)
     op = O.make_params(params.width, params.height, params.pf, params.max_lvl, lights=params.lights, flags=params.flags,
-                       seed=params.seed)
+                       seed=params.seed, corners=corners)   # (corners: the checked frame's view; None = the default)
     every = args.cpu_sample_every or wl.get("cpu_every", 96)
     threads = args.cpu_threads
 

@@ -91,6 +91,13 @@ __device__ float glibc_powf2(float x, const uint32_t *ties, int n) {
 // with glibc powf except where glibc itself is not correctly rounded (colour-only, <= 1 LSB).
 __device__ __forceinline__ float spec_powf(float x, float y) { return spec_pow(x, y); }
 
+// popcount(m & lanes below this lane): the lane's rank among the lanes of m below it (v_mbcnt_lo/hi:
+// two instructions, no 64-bit lane mask to make or keep live)
+__device__ __forceinline__ int rank_below(unsigned long long m) {
+    return static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
+}
+
 // Block-wide reservation in an output queue for kPer coalesced rounds of items: round k covers
 // items base + k*BLOCK + threadIdx.x, so reads and writes stay coalesced and the output keeps
 // input order. One atomicAdd per block chunk: a single counter word takes only ~88 atomics/us
@@ -115,10 +122,9 @@ __device__ __forceinline__ void block_reserve_rounds(const bool (&valid)[PER], i
     }
     __syncthreads();
     const int base = s_c[PER * NW];
-    const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
     for (int k = 0; k < PER; ++k)
-        pos[k] = valid[k] ? base + s_c[k * NW + wid] + __popcll(m[k] & below) : -1;
+        pos[k] = valid[k] ? base + s_c[k * NW + wid] + rank_below(m[k]) : -1;
     __syncthreads();
 }
 
@@ -839,8 +845,7 @@ __device__ __forceinline__ void bvh4_query_steal(const DevScene &sc, V3 o, V3 di
         const uint64_t donors = __ballot(owner >= 0 && sp - base >= 1);
         if (__popcll(idle) >= RT_STEAL_MIN_IDLE && donors) {
             const int np = min(__popcll(idle), __popcll(donors));
-            const uint64_t lt = (1ull << lane) - 1ull;
-            const int ir = __popcll(idle & lt), dr = __popcll(donors & lt);
+            const int ir = rank_below(idle), dr = rank_below(donors);
             if (((donors >> lane) & 1ull) && dr < np) {
                 s_xfer[wb + 2 * dr] = lane | (owner << 8);
                 if (RT_STEAL_TOP) {   // the top entry: the nearest subtree still pending
@@ -1115,7 +1120,9 @@ __device__ __forceinline__ Segment xcd_segment(int n, int block_dim, bool split)
     const int xcd = blockIdx.x % nseg;
     const int per_xcd_blocks = (static_cast<int>(gridDim.x) - 1 - xcd) / nseg + 1;   // blocks with this residue
     const int local = blockIdx.x / nseg;
-    const int chunk = (n + nseg - 1) / nseg;
+    // (whole 64-query chunks: every wave's range starts on a multiple of 64, so a wave's query indices
+    // j0 .. j0 + 63 share j0 >> 6 in every distribution, which the chain kernel reads as a scalar)
+    const int chunk = ((n + nseg - 1) / nseg + kWave - 1) & ~(kWave - 1);
     Segment g;
     g.begin = min(n, xcd * chunk);
     g.end = min(n, g.begin + chunk);
@@ -1192,8 +1199,8 @@ struct QueryCursor {
             const int g = blockIdx.x % nx;
             const int wpb = static_cast<int>(blockDim.x) / kWave;
             int c;
-            if (k == 0) {
-                c = static_cast<int>(blockIdx.x / nx) * wpb + static_cast<int>(threadIdx.x) / kWave;
+            if (k == 0) {   // (the wave's index in its block, as a scalar: the task index stays in SGPRs)
+                c = static_cast<int>(blockIdx.x / nx) * wpb + __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
                 k = 1;
             } else {
                 const int nblk = (static_cast<int>(gridDim.x) - 1 - g) / nx + 1;   // blocks of this sequence
@@ -2024,7 +2031,7 @@ __device__ __forceinline__ Secondary chain_step(const DevScene &sc, const ShadeP
             nh = __popcll(hm);
             G = nh ? min(p.n_lights - 1, (kWave - nh) / nh) : 0;   // (wave-uniform)
             if (G > 0) {
-                rk = __popcll((hit ? hm : ~hm) & ((1ull << lane) - 1ull));   // rank among the hit (other) lanes
+                rk = rank_below(hit ? hm : ~hm);   // rank among the hit (other) lanes
                 // lane k receives the hit lane of rank k and the other lane of rank k (lane 63 takes the
                 // unused writes: with G > 0 fewer than 64 lanes are of either kind); every lane runs the
                 // permutes, which read nothing from a masked lane
@@ -2290,7 +2297,6 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
     const int lane = __lane_id();
     const int spp = kInLane ? fuse_spp : 1, ppb = spb / spp;   // sample lanes per pixel, pixels per batch
     // pixel base lane of this lane's sample (fused launches): the first lane of its spp-lane group
-    const int pix_lane = kInLane ? ((fuse_spp & (fuse_spp - 1)) == 0 ? (lane & ~(fuse_spp - 1)) : lane - lane % fuse_spp) : 0;
     // distribution 4 (fused launches): wave tasks dealt round-robin to the XCDs and taken one at a
     // time from per-XCD counters in the (self-reset) counter buffer by a resident grid, so no wave
     // slot waits for the other waves of its block to retire; in batch order when ordered
@@ -2325,7 +2331,10 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         const DevScene &scb = sc;
         const DevWork &wb = w;
 #endif
-        const int vball = j0 >> 6;   // this wave's virtual batch (wave-uniform for the orderable distributions)
+        // this wave's virtual batch: wave-uniform in every distribution (xcd_segment hands out whole
+        // 64-query chunks), so it and everything derived from it (frame, batch, split tier, part, the
+        // order's entry) live in scalar registers
+        const int vball = __builtin_amdgcn_readfirstlane(j0 >> 6);
         const int fr = nfr > 1 ? vball % nfr : 0, vb = nfr > 1 ? vball / nfr : vball;   // (its frame, its batch in it)
         // the frame's outputs, read where they are written (held from the batch's start, they stayed live
         // through the chain and spilled), and its corner rays
@@ -2436,6 +2445,14 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
                 o[0] = rgb.x; o[1] = rgb.y; o[2] = rgb.z;
             }
         } else if (kInLane) {   // k_frame's arithmetic: a pixel's fuse_spp sub-samples sit in adjacent lanes
+            // (the pixel's first lane and the divisor made here from the argument, not at the kernel's start:
+            // held across the batch they were spilled to scratch and reloaded per batch)
+#if RT_OPAQUE_ARGS
+            KargPtr kf = (KargPtr)__builtin_amdgcn_kernarg_segment_ptr();
+            asm volatile("" : "+s"(kf));
+            const int fuse_spp = kf->fuse_spp;
+#endif
+            const int pix_lane = (fuse_spp & (fuse_spp - 1)) == 0 ? (lane & ~(fuse_spp - 1)) : lane - lane % fuse_spp;
             V3 acc = mk(0, 0, 0);
             for (int sub = 0; sub < fuse_spp; ++sub)   // summed in sub-sample order (main.cpp:377-391)
                 acc = add(acc, mk(__shfl(rgb.x, pix_lane + sub), __shfl(rgb.y, pix_lane + sub), __shfl(rgb.z, pix_lane + sub)));

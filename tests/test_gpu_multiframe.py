@@ -69,12 +69,13 @@ def test_frames_in_one_launch_equal_single_frames(name, knobs, workdir, gpu_avai
 def test_multiframe_workspace_grows_by_the_deep_records_only(workdir, gpu_available):
     """eight views at the reference's defaults (max_lvl 10: chain records past the three
     LDS steps) in one launch keep each frame's deep records at sample + frame x samples in chain_local;
-    only that array grows with the frames (7 more frames x 2.25M samples x 11 steps x 16 B), not the
+    only that array grows with the frames (7 more frames x 2.36M samples x 11 steps x 16 B), not the
     whole ~1 GB per-frame workspace (~8.5 GB before), and the call renders in one launch (no fallback)."""
     import torch
     dev = torch.device("cuda", 0)
     views = _views(REF, 8)
-    cap, steps = REF["w"] * REF["h"] * REF["pf"] ** 2, REF["max_lvl"] + 1
+    # (the workspace's samples: whole 16 x 16 tiles, the frame's edge tiles padded)
+    cap, steps = ((REF["w"] + 15) // 16) * ((REF["h"] + 15) // 16) * 256 * REF["pf"] ** 2, REF["max_lvl"] + 1
     with R.Scene.load(scene_path(REF["spec"], workdir), device=0) as sc:
         one, _ = _single(sc, torch, dev, views[7])
         torch.cuda.synchronize(dev)

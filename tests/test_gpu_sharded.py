@@ -76,7 +76,9 @@ def test_strong_shares_settled_reassemble_to_the_frame(knobs, workdir, gpu_avail
         total = np.zeros(3, np.uint64)
         for r in range(N):
             part = gathered[r * shard:(r + 1) * shard]
-            n = 0
+            sc.render_tiles_device(p, 16, 16, r, N, part.data_ptr(), part.numel(), stream)   # (resets the trials)
+            torch.cuda.synchronize()
+            n = 1
             while n < 64 and sc.trials()["choice"] < 0:
                 sc.render_tiles_device(p, 16, 16, r, N, part.data_ptr(), part.numel(), stream)
                 torch.cuda.synchronize()

@@ -11,6 +11,8 @@
 #   rocprof      rocprofv3 --kernel-trace --stats of the bench's timed entry point + trace summary
 #   workloads    tools/gpu_workloads.sh TAG (the other BASELINE workloads)
 #   e2e          bench.py --e2e-only: render -> host -> PPM per C4 frame
+#   ab           same-box A/B of library builds (AB_LIBS: names of raytracert_amd/ab/lib_<name>.so, 'cur' = the
+#                in-tree build; AB_PASSES; AB_WORKLOADS; AB_ARGS extra bench arguments): the timed loop only
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 TAG=$1; shift
@@ -56,6 +58,18 @@ for STEP in "$@"; do
     e2e)
       timeout -k 10 300 python bench.py --e2e-only > gpurun_out/e2e_$TAG.json 2> gpurun_out/e2e_$TAG.err || fail e2e gpurun_out/e2e_$TAG.err
       cat gpurun_out/e2e_$TAG.json ;;
+    ab)
+      for P in $(seq 1 ${AB_PASSES:-2}); do
+        for W in ${AB_WORKLOADS:-c4}; do
+          for L in ${AB_LIBS:-cur}; do
+            LIBV=""; [ "$L" != "cur" ] && LIBV=raytracert_amd/ab/lib_$L.so
+            R=$(RTAMD_LIB=$LIBV timeout -k 10 300 python bench.py --workload $W --no-cpu --no-bf-roofline --no-cold --no-path-compare \
+                --no-dropin --no-strong-shares --no-e2e --orbit-step 0 --no-multi-frame ${AB_ARGS:-} 2>gpurun_out/ab_$TAG.err) || fail ab gpurun_out/ab_$TAG.err
+            echo "$R" >> gpurun_out/ab_$TAG.jsonl
+            echo "$R" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); c=d["config"]; b=d.get("batches") or {}; print(sys.argv[1], sys.argv[2], "pass", sys.argv[3], d["ms_per_step"], "ms", "one", (c.get("one_in_flight") or {}).get("ms_per_step"), "in_flight", (c.get("in_flight") or {}).get("ms_per_step"), "chain", d["roofline"]["avg_launch_ms"], "batch max", b.get("max_us"))' $W $L $P
+          done
+        done
+      done ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
 done
