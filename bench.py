@@ -113,9 +113,11 @@ def parse():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c4")
     ap.add_argument("--no-bf-roofline", action="store_true", help="skip the brute-force kernel's roofline frame")
     ap.add_argument("--pipes", type=int, default=1, help="render pipelines a call's batches overlap on")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="N=1 frame path: frames in flight (RT_TUNE_FRAMES_IN_FLIGHT), consecutive frames "
-                         "on this many alternating streams into their own buffers")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="N=1 frame path: calls in flight (RT_TUNE_FRAMES_IN_FLIGHT), consecutive calls on this many "
+                         "alternating streams into their own buffers (r06: 1; with the camera path's distinct views, two "
+                         "four-view calls in flight measured 0.339-0.347 ms per frame against 0.331-0.332 one call at a "
+                         "time, profiles/r06e_ab_headline.txt)")
     ap.add_argument("--orbit-step", type=float, default=0.25,
                     help="N=1: also time a moving view, each frame the view turned by this many degrees more "
                          "(scenes.orbit_corners; 0 = skip): config.orbit")
@@ -131,7 +133,7 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true", help="N=1: skip the end-to-end frame (render -> host -> PPM file)")
     ap.add_argument("--e2e-only", action="store_true", help="N=1: only the end-to-end frame leg (one JSON line)")
     ap.add_argument("--e2e-frames", type=int, default=40, help="frames of the end-to-end leg per mode")
-    ap.add_argument("--ppm-threads", type=int, default=8, help="end-to-end leg: threads writing each PPM (rt_write_ppm_threads)")
+    ap.add_argument("--ppm-threads", type=int, default=8, help="end-to-end leg: threads writing each PPM (rt_ppm_writer)")
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
                     help="extra launch-shape knob (Scene.tune), e.g. shadow_virtual=-1; repeatable")
     return ap.parse_args()
@@ -1029,29 +1031,34 @@ def strong_shares(scene, cparams, W, H, dev, ns=(2, 4, 8), reps=15, warm=12, pip
     return out
 
 
-def end_to_end(scene, cparams, W, H, dev, frames=40, threads=8, workdir=None):
+def end_to_end(scene, cparams, W, H, dev, frames=40, threads=8, workdir=None, inflight=2):
     """A frame as the reference's 'r' key ends it (main.cpp:347-405): the render, the bytes in host
     memory (Image::_image's quantised bytes; here one device-to-host copy of the uint8 frame into pinned
-    memory), then writeImage("result.ppm") (rt_write_ppm_threads, `threads` writers, the same file as
-    rt_write_ppm; rt_write_ppm with one thread timed beside it). Two modes over `frames` frames:
+    memory), then writeImage("result.ppm") (rt_ppm_writer: the file kept mapped, `threads` threads copy
+    the frame in; the same file as rt_write_ppm, which is timed beside it). Two modes over `frames` frames:
     one at a time (render, copy, write in sequence, each synchronised) and pipelined (frame i's copy on
-    a copy stream and its PPM write on the host overlap frame i + 1's render). Host wall clock."""
+    a copy stream and its PPM write on the host overlap frame i + 1's render, the renders `inflight`
+    frames in flight on alternating streams, RT_TUNE_FRAMES_IN_FLIGHT). Host wall clock."""
     import numpy as np
     import torch
 
     import raytracert_amd as R
     st = torch.cuda.current_stream(dev)
     cs = torch.cuda.Stream(dev)
+    rs = [st] + [torch.cuda.Stream(dev) for _ in range(max(1, inflight) - 1)]   # render streams
     n = H * W * 3
     fbs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(2)]
     hbs = [torch.empty(n, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
     path = os.path.join(workdir or tempfile.mkdtemp(prefix="rt_e2e_"), "result.ppm")
+    path1 = os.path.join(os.path.dirname(path), "result_fwrite.ppm")
+    writer = R.PpmWriter(path, W, H, threads)
     ev_r = [torch.cuda.Event() for _ in range(2)]
     ev_c = [torch.cuda.Event() for _ in range(2)]
 
-    def render(i):
-        scene.render_frame_device(cparams, TILE, TILE, fbs[i % 2].data_ptr(), n, st.cuda_stream)
-        ev_r[i % 2].record(st)
+    def render(i, k=1):
+        s_ = rs[i % k]
+        scene.render_frame_device(cparams, TILE, TILE, fbs[i % 2].data_ptr(), n, s_.cuda_stream)
+        ev_r[i % 2].record(s_)
 
     def copy(i):
         cs.wait_event(ev_r[i % 2])
@@ -1059,12 +1066,12 @@ def end_to_end(scene, cparams, W, H, dev, frames=40, threads=8, workdir=None):
             hbs[i % 2].copy_(fbs[i % 2], non_blocking=True)
         ev_c[i % 2].record(cs)
 
-    def write(i, nt=threads):
+    def write(i):
         ev_c[i % 2].synchronize()
-        R.write_ppm_ptr(path, W, H, hbs[i % 2].data_ptr(), nt)
+        writer.write_ptr(hbs[i % 2].data_ptr())
 
     # one at a time: each stage waits for the one before it (a host that renders, reads and saves)
-    parts = {"render": [], "copy": [], "write": [], "write_1thread": []}
+    parts = {"render": [], "copy": [], "write": [], "write_fwrite": []}
     for i in range(frames + 3):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
@@ -1076,7 +1083,7 @@ def end_to_end(scene, cparams, W, H, dev, frames=40, threads=8, workdir=None):
         t2 = time.perf_counter()
         write(i)
         t3 = time.perf_counter()
-        R.write_ppm_ptr(path, W, H, hbs[i % 2].data_ptr(), 1)
+        R.write_ppm(path1, hbs[i % 2].numpy().reshape(H, W, 3))   # (rt_write_ppm: fopen + fwrite, one thread)
         t4 = time.perf_counter()
         if i >= 3:
             for k, v in zip(parts, (t1 - t0, t2 - t1, t3 - t2, t4 - t3)):
@@ -1085,29 +1092,37 @@ def end_to_end(scene, cparams, W, H, dev, frames=40, threads=8, workdir=None):
     one["ms_per_frame"] = round(one["render"] + one["copy"] + one["write"], 4)
     # pipelined: frame i's copy and write overlap frame i + 1's render
     def pipelined(count):
+        k = len(rs)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for i in range(count):
             if i >= 2:
-                st.wait_event(ev_c[i % 2])   # (frame i reuses frame i - 2's device buffer)
-            render(i)
+                rs[i % k].wait_event(ev_c[i % 2])   # (frame i reuses frame i - 2's device buffer)
+            render(i, k)
             copy(i)
             if i >= 1:
                 write(i - 1)
         write(count - 1)
         torch.cuda.synchronize(dev)
         return time.perf_counter() - t0
-    pipelined(4)
+    if len(rs) > 1:
+        scene.tune("frames_in_flight", len(rs))
+    pipelined(4 * len(rs))
     el = pipelined(frames)
+    scene.tune("frames_in_flight", 1)
+    writer.close()
     with open(path, "rb") as f:   # the last frame's file is the last frame's bytes
         body = f.read()
     ok = body[:len(f"P6\n{W} {H}\n255\n")] == f"P6\n{W} {H}\n255\n".encode() and \
         np.array_equal(np.frombuffer(body, np.uint8, offset=len(body) - n), fbs[(frames - 1) % 2].cpu().numpy())
     return {"what": "render -> uint8 frame in host memory (pinned, one device-to-host copy) -> result.ppm "
-                    "(rt_write_ppm_threads), as main.cpp:347-405 ends a frame; host wall clock, medians",
+                    "(rt_ppm_writer: the file kept mapped, the frame copied in by ppm_threads threads; write_fwrite = "
+                    "rt_write_ppm, fopen + fwrite, for comparison), as main.cpp:347-405 ends a frame; host wall clock, "
+                    "medians",
             "frames": frames, "ppm_threads": threads, "one_at_a_time": one,
-            "pipelined": {"ms_per_frame": round(el / frames * 1e3, 4),
-                          "what": "frame i's copy (copy stream) and PPM write (host) overlap frame i + 1's render"},
+            "pipelined": {"ms_per_frame": round(el / frames * 1e3, 4), "renders_in_flight": len(rs),
+                          "what": "frame i's copy (copy stream) and PPM write (host) overlap frame i + 1's render; "
+                                  "consecutive renders on alternating streams (RT_TUNE_FRAMES_IN_FLIGHT)"},
             "last_file_equals_frame": bool(ok)}
 
 

@@ -25,7 +25,7 @@
  *   rt_comm_*             RCCL communicator for it          (one process or host thread per GPU)
  *   rt_default_corners    produceRay for the 4 corners      main.cpp:300-325,355-358 (+ reshape :288-296)
  *   rt_write_ppm          Image::writeImage                 main.cpp:102-128
- *   rt_write_ppm_threads  the same file, the body written by several threads (end-to-end frames)
+ *   rt_ppm_writer_*       the same file, kept mapped for a frame per 'r' press    main.cpp:405
  *
  * Errors: the reference has none (loadMesh returns true always, mesh.cpp:330; a missing OBJ
  * crashes at fclose(NULL), mesh.cpp:329). Here every entry returns RT_OK (0) or a negative
@@ -294,11 +294,15 @@ int rt_assemble_tiles_device(int32_t device, int32_t width, int32_t height, int3
 int rt_default_corners(int32_t width, int32_t height, float corners[8][3]);
 /* Image::writeImage: "P6\n%i %i\n255\n" + w*h*3 bytes. */
 int rt_write_ppm(const char *path, int32_t width, int32_t height, const uint8_t *rgb_u8);
-/* The same file as rt_write_ppm (main.cpp:102-128, `writeImage("result.ppm")` at main.cpp:405), its
- * body written in `threads` slices side by side (pwrite; 1-256 threads), over the previous file's
- * pages when it exists (no truncation before the write; the size is set after). For hosts that write
- * a PPM per frame: one thread copies ~5-10 GB/s into the page cache, ~1 ms for a 1920x1080 frame. */
-int rt_write_ppm_threads(const char *path, int32_t width, int32_t height, const uint8_t *rgb_u8, int32_t threads);
+/* A host that writes result.ppm after every frame (main.cpp:405): the file opened once, sized and kept
+ * mapped; rt_ppm_writer_write copies a frame's w*h*3 bytes into it with `threads` threads (1-256), slice
+ * by slice, and returns when they are in the file's page-cache pages. The file then holds the bytes
+ * rt_write_ppm writes. (write() of one file does not scale with threads: the kernel serialises buffered
+ * writes to one inode.) */
+typedef struct rt_ppm_writer rt_ppm_writer;
+int rt_ppm_writer_open(const char *path, int32_t width, int32_t height, int32_t threads, rt_ppm_writer **out);
+int rt_ppm_writer_write(rt_ppm_writer *w, const uint8_t *rgb_u8);
+void rt_ppm_writer_close(rt_ppm_writer *w);
 
 /* ---- acceleration ------------------------------------------------------ */
 /* The reference loops over every triangle for every ray (raytracing.cpp:174-189) and leaves its

@@ -8,7 +8,7 @@ orchestration (torch.distributed over RCCL).
 """
 from ._capi import ALL_FEATURES, RtError, RT_HOST_ONLY  # noqa: F401
 from .api import (Comm, RenderParams, Scene, assemble_tiles_device, default_corners, device_count,  # noqa: F401
-                  load_mtl, ray_intersect_triangle, write_ppm, write_ppm_ptr)
+                  load_mtl, ray_intersect_triangle, write_ppm, PpmWriter)
 
-__all__ = ["Scene", "RenderParams", "Comm", "assemble_tiles_device", "default_corners", "write_ppm", "write_ppm_ptr", "device_count", "ray_intersect_triangle", "load_mtl", "RtError",
+__all__ = ["Scene", "RenderParams", "Comm", "assemble_tiles_device", "default_corners", "write_ppm", "PpmWriter", "device_count", "ray_intersect_triangle", "load_mtl", "RtError",
            "ALL_FEATURES", "RT_HOST_ONLY"]

@@ -123,7 +123,9 @@ _SIGNATURES = {
                                 C.c_size_t, _VP, C.POINTER(C.c_int32), _VP], C.c_int),
     "rt_default_corners": ([C.c_int32, C.c_int32, _VP], C.c_int),
     "rt_write_ppm": ([C.c_char_p, C.c_int32, C.c_int32, _VP], C.c_int),
-    "rt_write_ppm_threads": ([C.c_char_p, C.c_int32, C.c_int32, _VP, C.c_int32], C.c_int),
+    "rt_ppm_writer_open": ([C.c_char_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(_VP)], C.c_int),
+    "rt_ppm_writer_write": ([_VP, _VP], C.c_int),
+    "rt_ppm_writer_close": ([_VP], None),
     "rt_set_profiling": ([_VP, C.c_int32], C.c_int),
     "rt_kernel_stats": ([_VP, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.POINTER(C.c_double)], C.c_int),
     "rt_reset_stats": ([_VP], C.c_int),

@@ -37,10 +37,41 @@ def write_ppm(path: str, rgb_u8: np.ndarray) -> None:
     check(lib().rt_write_ppm(path.encode(), w, h, _ptr(rgb)))
 
 
-def write_ppm_ptr(path: str, width: int, height: int, host_ptr: int, threads: int = 1) -> None:
-    """rt_write_ppm_threads from a host address (e.g. a pinned torch tensor's data_ptr()): the same
-    file as write_ppm, written by `threads` threads."""
-    check(lib().rt_write_ppm_threads(path.encode(), width, height, C.c_void_p(host_ptr), threads))
+class PpmWriter:
+    """rt_ppm_writer_*: result.ppm written after every frame (main.cpp:405), the file kept mapped and
+    each frame's bytes copied in by `threads` threads; the file holds write_ppm's bytes."""
+
+    def __init__(self, path: str, width: int, height: int, threads: int = 8):
+        self._h = C.c_void_p()
+        self.width, self.height = width, height
+        check(lib().rt_ppm_writer_open(path.encode(), width, height, threads, C.byref(self._h)))
+
+    def write_ptr(self, host_ptr: int) -> None:
+        """The frame at a host address (e.g. a pinned torch tensor's data_ptr()), width*height*3 bytes."""
+        check(lib().rt_ppm_writer_write(self._h, C.c_void_p(host_ptr)))
+
+    def write(self, rgb_u8: np.ndarray) -> None:
+        rgb = np.ascontiguousarray(rgb_u8, np.uint8)
+        if rgb.size != self.width * self.height * 3:
+            raise ValueError("frame size differs from the writer's")
+        self.write_ptr(rgb.ctypes.data)
+
+    def close(self) -> None:
+        if self._h:
+            lib().rt_ppm_writer_close(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 @dataclass

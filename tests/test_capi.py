@@ -49,25 +49,23 @@ def test_write_ppm_roundtrip(tmp_path):
 
 
 @pytest.mark.parametrize("threads", [1, 3, 16])
-def test_write_ppm_threads_same_file(tmp_path, threads):
-    """rt_write_ppm_threads writes rt_write_ppm's file byte for byte, also over a larger previous
-    file (the size is set after the write) and a smaller one."""
+def test_ppm_writer_same_file(tmp_path, threads):
+    """rt_ppm_writer_* (a mapped result.ppm written after every frame) leaves rt_write_ppm's file byte
+    for byte, frame after frame, also over a larger previous file (sized at open)."""
     rng = np.random.default_rng(threads)
-    img = rng.integers(0, 256, (270, 480, 3), dtype=np.uint8)
     a, b = str(tmp_path / "a.ppm"), str(tmp_path / "b.ppm")
-    R.write_ppm(a, img)
     with open(b, "wb") as f:
-        f.write(b"x" * (img.size + 5000))
-    R.write_ppm_ptr(b, 480, 270, img.ctypes.data, threads)
-    assert open(a, "rb").read() == open(b, "rb").read()
-    small = img[:100]
-    R.write_ppm_ptr(b, 480, 100, np.ascontiguousarray(small).ctypes.data, threads)
-    R.write_ppm(a, small)
-    assert open(a, "rb").read() == open(b, "rb").read()
-    R.write_ppm_ptr(b, 480, 270, img.ctypes.data, threads)   # and back up to the larger frame
-    assert np.array_equal(read_ppm(b), img)
+        f.write(b"x" * (480 * 270 * 3 + 5000))
+    with R.PpmWriter(b, 480, 270, threads) as w:
+        for _ in range(3):
+            img = rng.integers(0, 256, (270, 480, 3), dtype=np.uint8)
+            w.write(img)
+            R.write_ppm(a, img)
+            assert open(a, "rb").read() == open(b, "rb").read()
+        with pytest.raises(ValueError):
+            w.write(img[:100])
     with pytest.raises(R.RtError):
-        R.write_ppm_ptr(b, 480, 270, img.ctypes.data, 0)
+        R.PpmWriter(b, 480, 270, 0)
 
 
 def test_errors_are_codes_with_messages(tmp_path):
