@@ -592,9 +592,7 @@ struct TraceState {
     }
     // The same test against the live globals, without copying them: every comparison folded into one
     // word (no branch per global: this runs once per performRayTracing call of the 'r' loop).
-    // (inlined into the cached call path: out of line, the call and its register saves cost as much as
-    // the compares)
-    __attribute__((always_inline)) bool matches_globals() const {
+    bool matches_globals() const {
         uint32_t x = static_cast<uint32_t>(scene != rtamd_dropin::scene()) | static_cast<uint32_t>(gen != scene_generation()) |
                      static_cast<uint32_t>(amb != Ambient) | static_cast<uint32_t>(dif != Diffuse) |
                      static_cast<uint32_t>(refl != Reflection) | static_cast<uint32_t>(sha != Shadows) |
@@ -648,7 +646,7 @@ struct FrameCache {
     Vec3Df c[8];                  // this frame's corner rays (produceRay) and divisors
     float divX = 0, divY = 0;
     ~FrameCache() { rt_host_free(rec); }
-    __attribute__((always_inline)) bool matches(const Vec3Df &o, const Vec3Df &d) const {   // the call's ray is record `next`'s, bit for bit
+    bool matches(const Vec3Df &o, const Vec3Df &d) const {   // the call's ray is record `next`'s, bit for bit
         const float *r = rec + 9 * next;
         return (TraceState::diff3(o.p, r) | TraceState::diff3(d.p, r + 3)) == 0;
     }

@@ -1206,7 +1206,7 @@ struct QueryCursor {
                 const int nblk = (static_cast<int>(gridDim.x) - 1 - g) / nx + 1;   // blocks of this sequence
                 int a = 0;
                 if (__lane_id() == 0) a = atomicAdd(&wq[g * kWqStride], 1);
-                c = nblk * wpb + __shfl(a, 0);
+                c = nblk * wpb + __builtin_amdgcn_readfirstlane(__shfl(a, 0));   // (a scalar: the wave's task)
             }
             const int b = ((((c >> glog) * nx + g) << glog) + (c & ((1 << glog) - 1))) * kWave;
             end = n;
@@ -1218,7 +1218,7 @@ struct QueryCursor {
             const int g = blockIdx.x % nx;
             int c = 0;
             if (__lane_id() == 0) c = atomicAdd(&wq[g * kWqStride], 1);
-            c = __shfl(c, 0);
+            c = __builtin_amdgcn_readfirstlane(__shfl(c, 0));
             const int b = ((((c >> glog) * nx + g) << glog) + (c & ((1 << glog) - 1))) * kWave;
             end = n;
             if (b < n) { j = b + __lane_id(); return true; }
@@ -1233,7 +1233,7 @@ struct QueryCursor {
                 end = min(n, begin + chunk);
                 int b = 0;
                 if (__lane_id() == 0) b = atomicAdd(&wq[g * kWqStride], kWave);
-                b = begin + __shfl(b, 0);
+                b = begin + __builtin_amdgcn_readfirstlane(__shfl(b, 0));
                 if (b < end) { j = b + __lane_id(); return true; }
                 ++k;
             }
@@ -2365,7 +2365,10 @@ __global__ __launch_bounds__(kBvhBlock) __attribute__((amdgpu_waves_per_eu(kStea
         }
         const int plen = ((ppb + nparts - 1) / nparts) * spp;   // whole pixels per part
         const bool wave_on = (vball << 6) < vend;
-        const int pb = (ordered && wave_on) ? wb.batch_order[ob] : vb;
+        // the batch of this wave task: a scalar load of the order (written by other launches only; read
+        // through a vector load its value was held in a VGPR across the batch and spilled)
+        const int pb = (ordered && wave_on)
+                           ? ((const __attribute__((address_space(4))) int32_t *)reinterpret_cast<uintptr_t>(wb.batch_order))[ob] : vb;
         const int lane_off = nparts > 1 ? part * plen + lane : (j0 & (kWave - 1));
         // (unordered, the XCD-segment distributions hand out unaligned ranges: the lane's own bound)
         const bool lane_on = (ordered ? wave_on : j0 < vend) && (nparts == 1 || lane < plen) && lane_off < spb;
