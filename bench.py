@@ -122,8 +122,9 @@ def parse():
                     help="N=1: also time a moving view, each frame the view turned by this many degrees more "
                          "(scenes.orbit_corners; 0 = skip): config.orbit")
     ap.add_argument("--no-multi-frame", action="store_true", help="skip the rt_render_frames_device leg")
-    ap.add_argument("--frames-per-call", type=int, default=4,
-                    help="N=1 frame path: frames per rt_render_frames_device call (one chain launch), 1-8")
+    ap.add_argument("--frames-per-call", type=int, default=8,
+                    help="N=1 frame path: frames per rt_render_frames_device call (one chain launch), 1-8 (r06: 8, "
+                         "0.320-0.322 ms per frame against 0.325-0.327 at 4, profiles/r06i_ab_views_per_call.txt)")
     ap.add_argument("--camera-path", type=float, default=0.25,
                     help="N=1 with --frames-per-call > 1: the frames of a call are consecutive views of a camera path "
                          "around the default view (turned -4..4 x this many degrees about y, a triangle wave of period "
@@ -370,8 +371,9 @@ def main():
     # steps' N frames in one launch, one gather, one un-permute), as the one-GPU line renders that many
     # frames per call; the step count must be a whole number of calls, else one step per call
     kstep = 1
-    if world > 1 and args.mode == "weak" and rtcomm is None and args.frames_per_call > 1 and args.steps % args.frames_per_call == 0:
-        kstep = min(args.frames_per_call, 8)
+    if world > 1 and args.mode == "weak" and rtcomm is None and args.frames_per_call > 1:
+        # the largest step count per call up to --frames-per-call that divides the timed steps
+        kstep = max(d for d in range(1, min(args.frames_per_call, 8) + 1) if args.steps % d == 0)
     main_run = Runner(world * kstep if args.mode == "weak" else 1, frame_path=world == 1 and rtcomm is None)
     main_run.kstep = kstep
     plan = main_run.plan
