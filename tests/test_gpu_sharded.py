@@ -211,11 +211,11 @@ def test_bench_multi_rank_rehearsal(tmp_path, gpu_available):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", "29533", os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2",
            "--warmup", "1", "--rehearse", "--workload", "c2", "--no-cpu", "--no-bf-roofline", "--no-cold",
-           "--no-path-compare"]
+           "--no-path-compare", "--frames-per-call", "1"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
-    assert d["n_gpus"] == 2 and d["config"]["frames_per_step"] == 2
+    assert d["n_gpus"] == 2 and d["config"]["frames_per_step"] == 2 and d["config"]["steps_per_call"] == 1
     assert d["rehearsal"]["frames_checked"] == 2 and d["rehearsal"]["all_equal_one_gpu_frame"]
     assert d["config"]["rays_per_step"] == 2 * 494405 and "strong" in d
 
