@@ -419,7 +419,8 @@ def main():
     if args.e2e_only:   # the end-to-end leg alone (tools/gpu_run.sh e2e)
         scene.tune("frames_in_flight", 1)
         calibrate(1)
-        e2e = end_to_end(scene, cparams, WIDTH, HEIGHT, dev, frames=args.e2e_frames, threads=args.ppm_threads, workdir=tmp)
+        e2e = {f"renders_in_flight_{k}": end_to_end(scene, cparams, WIDTH, HEIGHT, dev, frames=args.e2e_frames,
+                                                      threads=args.ppm_threads, workdir=tmp, inflight=k) for k in (1, 2)}
         if rank == 0:
             print(json.dumps({"metric": "end-to-end wall clock per frame", "workload": wl["desc"], "end_to_end": e2e}), flush=True)
         return
@@ -535,7 +536,8 @@ def main():
     # ---- end to end: render -> bytes in host memory -> result.ppm (main.cpp:347-405) ----
     e2e = None
     if world == 1 and not args.no_e2e and not args.rehearse:
-        e2e = end_to_end(scene, cparams, WIDTH, HEIGHT, dev, frames=args.e2e_frames, threads=args.ppm_threads, workdir=tmp)
+        e2e = end_to_end(scene, cparams, WIDTH, HEIGHT, dev, frames=args.e2e_frames, threads=args.ppm_threads, workdir=tmp,
+                         inflight=1)
         main_run.run(0, max(args.warmup, 3))
 
     # ---- the same work through the other path: N=1 the shard path (tiles + un-permute, what
