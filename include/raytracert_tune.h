@@ -130,6 +130,12 @@ extern "C" {
                                     static schedule (every RT_TUNE_ORDER_EVERY launches, undilated), 0-8.
                                     C4 orbit at 0.25 deg per frame, one in flight: r 1 0.456-0.461 ms, 2 0.50-0.52,
                                     3 0.54, 0 0.486 (profiles/r05h_orbit_ab.txt). Placement only */
+#define RT_TUNE_ORDER_EARLY 37    /* 1: a re-sorted batch order is taken by the very next launch when its sort
+                                    has already completed (hipEventQuery, no wait: frames one at a time, a moving
+                                    view's order then comes from the previous view, not the one before); 0
+                                    (default): always the launch after next (r02's double buffering). Measured
+                                    neutral: C4 orbit one at a time 0.430-0.432 ms either way, cold and static
+                                    frames equal (profiles/r06o_ab_order_early.txt). Placement only */
 #define RT_TUNE_TOP_NODES 13     /* retired in r03 (0-85 accepted, no effect): an LDS copy of the four-wide
                                     tree's top levels; with float node rows loaded from global memory it
                                     measured slower (flat loads, 64-bit addresses) */

@@ -53,6 +53,7 @@ TUNE_INFLIGHT_DYNAMIC = 33
 TUNE_INFLIGHT_STREAMS = 34
 TUNE_QUAD_WALK = 35
 TUNE_MOTION_ORDER = 36
+TUNE_ORDER_EARLY = 37
 MAX_FRAMES_PER_CALL = 8   # RT_MAX_FRAMES_PER_CALL
 BVH_INFO_FIELDS = 7
 STOCHASTIC = 1 << 8

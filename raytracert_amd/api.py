@@ -374,7 +374,7 @@ class Scene:
              "shadow_helpers": _capi.TUNE_SHADOW_HELPERS, "frames_in_flight": _capi.TUNE_FRAMES_IN_FLIGHT,
              "adopt_order": _capi.TUNE_ADOPT_ORDER, "inflight_dynamic": _capi.TUNE_INFLIGHT_DYNAMIC,
              "inflight_streams": _capi.TUNE_INFLIGHT_STREAMS, "quad_walk": _capi.TUNE_QUAD_WALK,
-             "motion_order": _capi.TUNE_MOTION_ORDER}[knob]
+             "motion_order": _capi.TUNE_MOTION_ORDER, "order_early": _capi.TUNE_ORDER_EARLY}[knob]
         check(lib().rt_scene_tune(self._h, k, int(value)))
 
     def workspace_bytes(self) -> tuple[int, int]:

@@ -127,7 +127,7 @@ def test_tune_knobs_validate_ranges(tmp_path):
                             ("cold_estimate", (0, 1, 2), (3, -1)),
                             ("steal_half", (0, 512, 65535), (-1, 65536)), ("steal_quarter", (-1, 0, 8, 4096), (-2, 4097)),
                             ("split_eighth", (0, 64, 4096), (-1, 4097)), ("prio_batches", (0, 64, 1 << 30), (-1,)),
-                            ("shadow_helpers", (0, 1, 2), (3, -1)), ("quad_walk", (0, 1), (2, -1)), ("motion_order", (0, 1, 2, 8), (9, -1)), ("frames_in_flight", (1, 2, 4), (0, 5)), ("pipes", (1, 4), (0, 5))]:
+                            ("shadow_helpers", (0, 1, 2), (3, -1)), ("quad_walk", (0, 1), (2, -1)), ("motion_order", (0, 1, 2, 8), (9, -1)), ("order_early", (0, 1), (2, -1)), ("frames_in_flight", (1, 2, 4), (0, 5)), ("pipes", (1, 4), (0, 5))]:
         for v in good:
             s.tune(knob, v)
         for v in bad:
