@@ -29,3 +29,19 @@ def test_strong_model_bounds():
         assert r["render_ms"] >= 0.38 and r["render_ms"] >= 0.39 / n
         for bw in ("50GBs", "150GBs"):
             assert r[bw]["pipelined_ms_per_frame"] <= r[bw]["latency_ms_per_frame"]
+
+
+def test_strong_model_takes_measured_shares():
+    """With strong_shares (r06) the render and un-permute terms are the measured ones: the slowest rank's
+    share one frame at a time (latency) and four frames' shares per call (pipelined)."""
+    shares = {f"n{n}": {"max_ms": 0.3 / n ** 0.5, "pipelined_max_ms": 0.33 / n, "assemble_ms": 0.007} for n in (2, 4, 8)}
+    m = bench.strong_model(0.36, 0.43, None, 1920 * 1080 * 3, shares=shares, t1_pipe_ms=0.323)
+    assert m["inputs"]["render"].startswith("measured")
+    for n in (2, 4, 8):
+        r = m[f"n{n}"]
+        assert r["render_ms"] == round(shares[f"n{n}"]["max_ms"], 4)
+        assert r["render_pipelined_ms"] == round(shares[f"n{n}"]["pipelined_max_ms"], 4)
+        assert r["assemble_ms"] == 0.007
+        lat = r["150GBs"]["latency_ms_per_frame"]
+        assert lat > r["render_ms"] + r["assemble_ms"]   # gather and barrier come on top
+        assert abs(r["150GBs"]["pipelined_speedup"] - 0.323 / r["150GBs"]["pipelined_ms_per_frame"]) < 0.02
