@@ -885,7 +885,11 @@ def orbit_leg(scene, run, W, H, PF, MAX_LVL, LIGHTS, flags, args, inflight, obj,
     import raytracert_amd as R
     from raytracert_amd import scenes
     warm, K = max(args.warmup, 2) * inflight, args.steps
-    corners = [scenes.orbit_corners(W, H, k + 1, args.orbit_step) for k in range(warm + K)]
+    fpc = args.frames_per_call if not args.no_multi_frame else 1
+    calls = max(K // fpc, 1)
+    # (enough views for the multi-frame calls below too: at small --steps a call holds more views than K)
+    nviews = max(warm + K, warm + calls * fpc, max(warm // fpc, 2) * fpc) if fpc > 1 else warm + K
+    corners = [scenes.orbit_corners(W, H, k + 1, args.orbit_step) for k in range(nviews)]
     views = [R.RenderParams(width=W, height=H, pf=PF, max_lvl=MAX_LVL, lights=LIGHTS, flags=flags, corners=c).to_c()
              for c in corners]
 
@@ -906,10 +910,8 @@ def orbit_leg(scene, run, W, H, PF, MAX_LVL, LIGHTS, flags, args, inflight, obj,
     el1 = loop(1, warm, K) if inflight > 1 else el
     # a camera path rendered --frames-per-call consecutive views per rt_render_frames_device call (one
     # chain launch over the views, one call at a time); the call's last view re-rendered alone must match
-    fpc = args.frames_per_call if not args.no_multi_frame else 1
     multi = None
     if fpc > 1:
-        calls = max(K // fpc, 1)
         scene.tune("frames_in_flight", 1)
         st = run.fstreams[0]
 

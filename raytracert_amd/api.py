@@ -280,6 +280,8 @@ class Scene:
         """rt_render_frames_device: len(params) views of one frame geometry (params differ in corners only),
         view f row-major into the device buffer out_ptrs[f], in one chain launch where possible."""
         n = len(params)
+        if len(out_ptrs) != n:
+            raise ValueError(f"render_frames_device: {n} views but {len(out_ptrs)} output buffers")
         arr = (RtParams * n)()
         keep = []
         for i, q in enumerate(params):
