@@ -171,6 +171,7 @@ const uint32_t *powf2_tie_table(size_t *n);
 // Error slot of the C-ABI (rt_last_error_string) for the library's other translation units, and
 // the device a scene is bound to (RT_HOST_ONLY for host-only scenes).
 int set_error(int code, const std::string &msg);
+int guard_failure() noexcept;   // inside a catch handler of a C entry: the exception as an RT_E_* code
 int scene_device(const rt_scene *s);
 
 }  // namespace rt

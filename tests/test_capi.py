@@ -188,3 +188,20 @@ def test_multiframe_and_reserve_entries_refuse_without_a_device(tmp_path):
     assert lib.rt_render_frames_device(None, C.byref(cp), 2, 16, 16, outs, 192, None, None) == _capi.RT_E_ARG
     assert lib.rt_scene_reserve(None, C.byref(cp), 16, 16, 0) == _capi.RT_E_ARG
     assert _capi.MAX_FRAMES_PER_CALL == 8
+
+
+def test_every_c_entry_is_exception_guarded():
+    """No C++ exception crosses the C ABI (a failed host allocation is RT_E_NOMEM, not std::terminate in
+    the host): every rt_* entry defined in the library's C-ABI sources runs its body in try/catch."""
+    import os
+    import re
+    src = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "raytracert_amd", "csrc")
+    seen = 0
+    for f in ("rt_capi.cpp", "rt_comm.cpp"):
+        text = open(os.path.join(src, f)).read()
+        for m in re.finditer(r"^(int|void) (rt_\w+)\([^;{]*\)\s*\{\n(\s*)(\S+)", text, re.M):
+            seen += 1
+            assert m.group(4) == "try", f"{f}: {m.group(2)} is not wrapped in try/catch"
+            body = text[m.end():text.find("\n}\n", m.end())]
+            assert "catch (...)" in body, f"{f}: {m.group(2)} has no catch (...)"
+    assert seen >= 50
