@@ -2778,6 +2778,51 @@ __global__ __launch_bounds__(kBlock) void k_assemble_pieces(const uint8_t *__res
     }
 }
 
+// The un-permute of a whole gather of 16x16 tiles into frames whose width is a multiple of 16, staged
+// through LDS so that both sides move whole lines: a block takes kAsmTiles consecutive tiles of one
+// frame's tile row, reads each from its rank's shard (768 contiguous bytes) into LDS and writes the 16
+// frame rows they cover as runs of kAsmTiles x 48 contiguous bytes. (k_assemble_pieces reads tile rows
+// in order but writes them as 48-byte pieces 5,760 bytes apart; here no store is narrower than a run.)
+#ifndef RT_ASM_ROWS
+#define RT_ASM_ROWS 1   // 0: every un-permute through k_assemble_pieces (A/B)
+#endif
+constexpr int kAsmTiles = 16;
+constexpr int kAsmTileBytes = 16 * 16 * 3;          // 768
+constexpr int kAsmLdsStride = kAsmTileBytes + 48;   // (a pad that spreads a row's three tile reads over banks)
+struct AssembleRowDivs { UDiv nranks, chunks, tiles_y; };
+__global__ __launch_bounds__(kBlock) void k_assemble_rows(const uint8_t *__restrict__ gathered, int32_t width, int32_t height,
+                                                          int32_t tiles_x, int32_t tiles_total, int32_t nranks, uint32_t nslots,
+                                                          AssembleRowDivs dv, uint8_t *__restrict__ out) {
+    __shared__ uint4 stage[kAsmTiles * kAsmLdsStride / 16];
+    // block -> (frame f, tile row ty, tile chunk c)
+    const uint32_t b = blockIdx.x;
+    const uint32_t fr = udiv(b, dv.chunks), c = b - fr * dv.chunks.d;
+    const uint32_t f = udiv(fr, dv.tiles_y), ty = fr - f * dv.tiles_y.d;
+    const int tx0 = static_cast<int>(c) * kAsmTiles;
+    const int ntiles = min(kAsmTiles, tiles_x - tx0);
+    // read: kAsmTiles x 48 pieces of 16 B, each tile's 48 from its rank's slot
+    for (int q = threadIdx.x; q < kAsmTiles * 48; q += kBlock) {
+        const int k = q / 48, w = q - k * 48;
+        if (k >= ntiles) continue;
+        const uint32_t g = f * static_cast<uint32_t>(tiles_total) + ty * static_cast<uint32_t>(tiles_x) + static_cast<uint32_t>(tx0 + k);
+        const uint32_t slot = udiv(g, dv.nranks), rank = g - slot * dv.nranks.d;
+        const int64_t tile = static_cast<int64_t>(rank) * nslots + slot;
+        stage[(k * kAsmLdsStride) / 16 + w] = reinterpret_cast<const uint4 *>(gathered + tile * kAsmTileBytes)[w];
+    }
+    __syncthreads();
+    // write: 16 frame rows of ntiles x 48 bytes
+    const int run = ntiles * 3;   // pieces of 16 B per row
+    for (int q = threadIdx.x; q < 16 * kAsmTiles * 3; q += kBlock) {
+        const int r = q / (kAsmTiles * 3), w = q - r * (kAsmTiles * 3);
+        const int y = static_cast<int>(ty) * 16 + r;
+        if (w >= run || y >= height) continue;
+        const int k = w / 3, part = w - 3 * k;
+        const uint4 v = stage[(k * kAsmLdsStride + r * 48) / 16 + part];
+        uint8_t *dst = out + ((static_cast<int64_t>(f) * height + y) * width + static_cast<int64_t>(tx0) * 16) * 3;
+        reinterpret_cast<uint4 *>(dst)[w] = v;
+    }
+}
+
 inline unsigned grid_for(int64_t n) { return static_cast<unsigned>((n + kBlock - 1) / kBlock); }
 
 }  // namespace
@@ -3156,6 +3201,17 @@ void launch_assemble_tiles(const uint8_t *gathered, int32_t width, int32_t heigh
     const int64_t rows = static_cast<int64_t>(nranks) * nslots * th;   // one thread per gathered tile row
     if (rows <= 0 || static_cast<int64_t>(frames) * width * height <= 0) return;
     const int64_t ppr = (static_cast<int64_t>(tw) * 3 + 15) / 16, npieces = rows * ppr;
+    const int32_t tiles_y = tiles_total / tiles_x;
+    const int64_t chunks = (tiles_x + kAsmTiles - 1) / kAsmTiles, blocks = static_cast<int64_t>(frames) * tiles_y * chunks;
+    if (RT_ASM_ROWS && tw == 16 && th == 16 && width % 16 == 0 && slot0 == 0 && nslots == slots &&
+        ((reinterpret_cast<uintptr_t>(gathered) | reinterpret_cast<uintptr_t>(out)) & 15) == 0 &&
+        static_cast<int64_t>(frames) * tiles_total < (int64_t(1) << 32) && blocks < (int64_t(1) << 31)) {
+        const AssembleRowDivs dv{make_udiv(static_cast<uint32_t>(nranks)), make_udiv(static_cast<uint32_t>(chunks)),
+                                 make_udiv(static_cast<uint32_t>(tiles_y))};
+        hipLaunchKernelGGL(k_assemble_rows, dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, stream, gathered, width, height,
+                           tiles_x, tiles_total, nranks, static_cast<uint32_t>(nslots), dv, out);
+        return;
+    }
     if (npieces < (int64_t(1) << 32) - kBlock && slot0 + nslots < (int64_t(1) << 32)) {
         const AssembleDivs dv{make_udiv(static_cast<uint32_t>(ppr)), make_udiv(static_cast<uint32_t>(th)),
                               make_udiv(static_cast<uint32_t>(nslots)), make_udiv(static_cast<uint32_t>(tiles_total)),

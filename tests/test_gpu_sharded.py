@@ -55,6 +55,47 @@ def test_assemble_composes_interleaved_shards(nranks, frames, size, tile, workdi
     assert [int(x) for x in total] == [frames * int(x) for x in c1]
 
 
+def _unpermute_reference(gathered, w, h, tile, frames, nranks):
+    """numpy restatement of the un-permute's layout: global tile g = f * T + t is held by rank g % N in
+    slot g / N; each tile is tile x tile x 3 bytes, clipped at the frame's right and bottom edges."""
+    tx_n, ty_n = (w + tile - 1) // tile, (h + tile - 1) // tile
+    T = tx_n * ty_n
+    slots = (frames * T + nranks - 1) // nranks
+    tiles = gathered.reshape(nranks, slots, tile, tile, 3)
+    out = np.zeros((frames, ty_n * tile, tx_n * tile, 3), np.uint8)
+    for g in range(frames * T):
+        f, t = divmod(g, T)
+        ty, tx = divmod(t, tx_n)
+        out[f, ty * tile:(ty + 1) * tile, tx * tile:(tx + 1) * tile] = tiles[g % nranks, g // nranks]
+    return out[:, :h, :w]
+
+
+@pytest.mark.parametrize("nranks,frames,size,tile,offset", [(3, 2, (176, 90), 16, 0), (8, 3, (800, 600), 16, 0),
+                                                            (8, 2, (1920, 1080), 16, 0), (1, 1, (256, 32), 16, 0),
+                                                            (7, 2, (800, 600), 16, 3), (4, 2, (500, 500), 16, 0),
+                                                            (5, 3, (64, 48), 8, 0)])
+def test_assemble_matches_the_layout_on_random_bytes(nranks, frames, size, tile, offset, gpu_available):
+    """rt_assemble_tiles_device against a numpy restatement of the layout, on random shard bytes: the
+    LDS-staged kernel (16x16 tiles, width a multiple of 16, whole gather, 16-B aligned buffers: partial
+    tile chunks, partial bottom tile rows, 1-8 ranks) and the per-piece kernel (other widths, 8x8 tiles,
+    an output 3 bytes off alignment) leave the same frames, and nothing outside them."""
+    import torch
+    w, h = size
+    T = ((w + tile - 1) // tile) * ((h + tile - 1) // tile)
+    slots = (frames * T + nranks - 1) // nranks
+    rng = np.random.default_rng(nranks * 1000 + w)
+    gathered = rng.integers(0, 256, nranks * slots * tile * tile * 3, dtype=np.uint8)
+    d_g = torch.from_numpy(gathered).to("cuda:0")
+    n = frames * h * w * 3
+    d_out = torch.full((n + offset + 64,), 7, dtype=torch.uint8, device="cuda:0")
+    stream = torch.cuda.current_stream().cuda_stream
+    R.assemble_tiles_device(0, w, h, tile, tile, frames, nranks, d_g.data_ptr(), d_g.numel(), d_out.data_ptr() + offset, n,
+                            stream)
+    got = d_out.cpu().numpy()
+    assert np.array_equal(got[offset:offset + n].reshape(frames, h, w, 3), _unpermute_reference(gathered, w, h, tile, frames, nranks))
+    assert (got[:offset] == 7).all() and (got[offset + n:] == 7).all()
+
+
 @pytest.mark.parametrize("knobs", [{}, {"split_eighth": 4096}, {"quad_walk": 1, "steal_quarter": 4096}])
 def test_strong_shares_settled_reassemble_to_the_frame(knobs, workdir, gpu_available):
     """bench.strong_shares' measurement: at N = 8 each rank's share of one C4 frame is
