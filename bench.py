@@ -39,6 +39,7 @@ VALU_CYCLES_PER_WAVE_INST = 4   # wave64 non-packed FP32 op on one SIMD (tools/v
 CLOCK_HZ = 2.4e9
 HBM_PEAK_GBS = 8000.0
 TILE = 16
+LEG_STEPS = 100   # frames the modes beside the headline time at least (one at a time, two in flight, the orbit)
 # BASELINE.json configs. C4 is the metric's configuration and the default; the
 # others are available with --workload (C1 is the reference's own CPU-only plumbing case).
 WORKLOADS = {
@@ -466,19 +467,23 @@ def main():
     one_in_flight = in_flight = None
     value_mode = (f"{fpc}_frames_per_call" if fpc > 1 else "") + (f"{'_' if fpc > 1 else ''}{inflight}_in_flight" if inflight > 1 else "")
     value_mode = (value_mode or "one_in_flight") + ("_camera_path" if timed_rays else "")
+    # (the modes beside the headline time at least LEG_STEPS frames, whatever --steps the headline takes: a run of
+    # 20 frames one at a time reads ~6% above the steady state, its first launch and last sync unamortised)
+    leg_steps = max(args.steps, LEG_STEPS)
     if main_run.single and (inflight > 1 or fpc > 1):   # the same frames one at a time (each frame's own latency)
         scene.tune("frames_in_flight", 1)
         main_run.fif = 1
-        el1, _ = main_run.run(args.steps, args.warmup)
-        one_in_flight = {"ms_per_step": round(el1 / args.steps * 1e3, 3),
-                         "value": round(rays_per_step * args.steps / el1 / 1e6, 4),
+        el1, _ = main_run.run(leg_steps, args.warmup)
+        one_in_flight = {"ms_per_step": round(el1 / leg_steps * 1e3, 3),
+                         "value": round(rays_per_step * leg_steps / el1 / 1e6, 4), "frames": leg_steps,
                          "what": "the same timed loop with one frame per call and one in flight (each launch waits for "
                                  "the previous frame)"}
         if fpc > 1:   # and one frame per call, two calls in flight on two streams (round 4's headline mode)
             scene.tune("frames_in_flight", 2)
             main_run.fif = 2
-            el2, _ = main_run.run(args.steps, args.warmup * 2)
-            in_flight = {"ms_per_step": round(el2 / args.steps * 1e3, 3), "value": round(rays_per_step * args.steps / el2 / 1e6, 4),
+            el2, _ = main_run.run(leg_steps, args.warmup * 2)
+            in_flight = {"ms_per_step": round(el2 / leg_steps * 1e3, 3), "value": round(rays_per_step * leg_steps / el2 / 1e6, 4),
+                         "frames": leg_steps,
                          "what": "one frame per call, two frames in flight on alternating streams (RT_TUNE_FRAMES_IN_FLIGHT 2)"}
             scene.tune("frames_in_flight", 1)
             main_run.fif = 1
@@ -858,7 +863,7 @@ def multiframe_leg(scene, run, cparams, W, H, args, rays_per_frame, dev):
                    "headline's calls render distinct camera-path views instead)"}
     for K, fif in ((2, 1), (4, 1), (8, 1), (2, 2), (4, 2)):
         scene.tune("frames_in_flight", fif)
-        calls = max(args.steps // K, 2)
+        calls = max(max(args.steps, LEG_STEPS) // K, 2)
 
         def call(i):
             st = run.fstreams[i % fif] if fif <= len(run.fstreams) else run.fstreams[0]
@@ -892,7 +897,7 @@ def orbit_leg(scene, run, W, H, PF, MAX_LVL, LIGHTS, flags, args, inflight, obj,
 
     import raytracert_amd as R
     from raytracert_amd import scenes
-    warm, K = max(args.warmup, 2) * inflight, args.steps
+    warm, K = max(args.warmup, 2) * inflight, max(args.steps, LEG_STEPS)
     fpc = args.frames_per_call if not args.no_multi_frame else 1
     calls = max(K // fpc, 1)
     # (enough views for the multi-frame calls below too: at small --steps a call holds more views than K)
