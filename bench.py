@@ -1201,6 +1201,17 @@ def timed_instantiation(kernel: str, name: str, multi: bool) -> bool:
     return len(targs) < 7 or targs[6] == ("true" if multi else "false")
 
 
+def profile_age(path: str):
+    """Sort key of a round-tagged profile name, oldest first: r06z_pmc.json < r06aa_pmc.json (a round's
+    tags run a..z, then aa, ab, ...; a plain string sort would put r06z after r06aa)."""
+    import re
+    m = re.match(r"r(\d+)([a-z0-9]*?)_", os.path.basename(path))
+    if not m:
+        return (-1, 0, os.path.basename(path))
+    tag = re.match(r"[a-z]*", m.group(2)).group(0)
+    return (int(m.group(1)), len(tag), m.group(2))
+
+
 def rocprof_mean(kernel: str, workload: str = "c4", multi: bool = False):
     """The committed rocprofv3 kernel-trace summary of `kernel` (tools/kernel_trace_summary.py over
     tools/gpu_final.sh's rocprof run of this bench, one frame in flight): the instantiation with the
@@ -1208,7 +1219,7 @@ def rocprof_mean(kernel: str, workload: str = "c4", multi: bool = False):
     import glob
     if workload != "c4":
         return None, None
-    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_kernel_trace_summary.json")), reverse=True):
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_kernel_trace_summary.json")), key=profile_age, reverse=True):
         try:
             ks = json.load(open(f)).get("kernels", {})
         except (OSError, ValueError):
@@ -1234,7 +1245,7 @@ def pmc_counters(kernel: str, need: str, workload: str = "c4", multi: bool = Fal
     summary of `workload` that has counter `need`: (dict, file) or (None, None)."""
     import glob
     suffix = "_pmc.json" if workload == "c4" else f"_pmc_{workload}.json"
-    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*" + suffix)))   # round-tagged names sort by age
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*" + suffix)), key=profile_age)   # oldest first
     for f in reversed(files):
         try:
             d = json.load(open(f))

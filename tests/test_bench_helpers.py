@@ -45,3 +45,13 @@ def test_strong_model_takes_measured_shares():
         lat = r["150GBs"]["latency_ms_per_frame"]
         assert lat > r["render_ms"] + r["assemble_ms"]   # gather and barrier come on top
         assert abs(r["150GBs"]["pipelined_speedup"] - 0.323 / r["150GBs"]["pipelined_ms_per_frame"]) < 0.02
+
+
+def test_profile_age_orders_round_tags():
+    """The roofline reads the newest committed profile: round-tagged names sort by round, then by tag
+    length, then by tag (r06z before r06aa: a plain string sort put r06z last and read a stale profile)."""
+    names = ["r06aa_pmc.json", "r05zf_pmc.json", "r06z_pmc.json", "r06_pmc.json", "r06am_pmc.json", "r06b_pmc.json",
+             "r02h_pmc.json"]
+    got = sorted(names, key=bench.profile_age)
+    assert got == ["r02h_pmc.json", "r05zf_pmc.json", "r06_pmc.json", "r06b_pmc.json", "r06z_pmc.json", "r06aa_pmc.json",
+                   "r06am_pmc.json"]
