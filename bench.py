@@ -88,6 +88,7 @@ def workload_scene(spec, workdir):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--e2e-inflight", type=int, default=1)   # renders in flight in the full line's end-to-end leg
     ap.add_argument("--steps", type=int, default=100)   # ~50 ms of C4 frames: fixed sync costs amortised
     ap.add_argument("--warmup", type=int, default=20)   # (the launch trials run before it: calibration)
     ap.add_argument("--mode", choices=("weak", "strong"), default="weak")
@@ -550,7 +551,7 @@ def main():
     e2e = None
     if world == 1 and not args.no_e2e and not args.rehearse:
         e2e = end_to_end(scene, cparams, WIDTH, HEIGHT, dev, frames=args.e2e_frames, threads=args.ppm_threads, workdir=tmp,
-                         inflight=1)
+                         inflight=args.e2e_inflight)
         main_run.run(0, max(args.warmup, 3))
 
     # ---- the same work through the other path: N=1 the shard path (tiles + un-permute, what
