@@ -88,7 +88,7 @@ def workload_scene(spec, workdir):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--e2e-inflight", type=int, default=1)   # renders in flight in the full line's end-to-end leg
+    ap.add_argument("--e2e-inflight", type=int, default=2)   # renders in flight in the full line's end-to-end leg (r06as: 0.37-0.48 vs 0.50-0.66 ms with one)
     ap.add_argument("--steps", type=int, default=100)   # ~50 ms of C4 frames: fixed sync costs amortised
     ap.add_argument("--warmup", type=int, default=20)   # (the launch trials run before it: calibration)
     ap.add_argument("--mode", choices=("weak", "strong"), default="weak")
