@@ -470,11 +470,11 @@ def main():
     value_mode = (value_mode or "one_in_flight") + ("_camera_path" if timed_rays else "")
     # (the modes beside the headline time at least LEG_STEPS frames, whatever --steps the headline takes: a run of
     # 20 frames one at a time reads ~6% above the steady state, its first launch and last sync unamortised)
-    leg_steps = max(args.steps, LEG_STEPS)
+    leg_steps, leg_warm = max(args.steps, LEG_STEPS), max(args.warmup, 20)
     if main_run.single and (inflight > 1 or fpc > 1):   # the same frames one at a time (each frame's own latency)
         scene.tune("frames_in_flight", 1)
         main_run.fif = 1
-        el1, _ = main_run.run(leg_steps, args.warmup)
+        el1, _ = main_run.run(leg_steps, leg_warm)
         one_in_flight = {"ms_per_step": round(el1 / leg_steps * 1e3, 3),
                          "value": round(rays_per_step * leg_steps / el1 / 1e6, 4), "frames": leg_steps,
                          "what": "the same timed loop with one frame per call and one in flight (each launch waits for "
@@ -482,7 +482,7 @@ def main():
         if fpc > 1:   # and one frame per call, two calls in flight on two streams (round 4's headline mode)
             scene.tune("frames_in_flight", 2)
             main_run.fif = 2
-            el2, _ = main_run.run(leg_steps, args.warmup * 2)
+            el2, _ = main_run.run(leg_steps, leg_warm * 2)
             in_flight = {"ms_per_step": round(el2 / leg_steps * 1e3, 3), "value": round(rays_per_step * leg_steps / el2 / 1e6, 4),
                          "frames": leg_steps,
                          "what": "one frame per call, two frames in flight on alternating streams (RT_TUNE_FRAMES_IN_FLIGHT 2)"}
